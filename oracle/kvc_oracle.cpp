@@ -1,0 +1,184 @@
+// kvc_oracle.cpp -- CPU restatement of the PyTorch CPU arithmetic that the reference's
+// kvcompress/methods hot path executes.  TEST INFRASTRUCTURE ONLY: this library is the checker
+// for the HIP engine.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+// load it; the product path (cs3602-llm-inference-acceleration_amd/kvcompress) never does.
+//
+// Parity pinning: tests/golden/*.npz were produced by the unmodified reference
+// (/root/reference/kvcompress, imported in the build container by tests/golden/gen_goldens.py);
+// tests/test_oracle_golden.py checks this restatement against every one of them.
+//
+// What is restated (reference call sites in brackets):
+//   * torch.norm(x, p=2, dim=-1) for fp32/bf16 rows          [methods/fix_size_l2.py:106,
+//     l2_compress.py:228, h2o_l2.py:296, snapkv_lite.py:96, pyramid_kv.py:313, adaptive_l2.py:473,527]
+//     = 8 fp32 lane accumulators, lane j: acc_j = fma(x[d], x[d], acc_j) for d = j, j+8, ...;
+//       serial lane sum ((a0+a1)+a2)+...+a7; correctly rounded fp32 sqrt; RNE to the storage dtype.
+//   * Tensor.argsort(dim=-1[, descending]) (stable=False)     [fix_size_l2.py:107,113 ...]
+//     = libstdc++ std::sort on (key, index) pairs with PyTorch's key-only comparators
+//       asc: (!isnan(a) && isnan(b)) || a < b        desc: (isnan(a) && !isnan(b)) || a > b
+//   * torch.topk(x, k, dim=-1) (largest, sorted)              [snapkv_lite.py:134]
+//     = std::partial_sort when k*64 <= n, else std::nth_element(k-1) + std::sort(first k-1),
+//       NaN-first '>' comparator (aten TopKImpl.h).
+//   * snapkv scoring: max(dim)+1e-6, subtraction, avg_pool1d(k, stride 1, pad k//2,
+//     count_include_pad)                                       [snapkv_lite.py:99-121]
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <utility>
+#include <vector>
+
+namespace {
+
+enum { DT_F32 = 0, DT_BF16 = 1 };
+
+inline float bf16_to_f32(uint16_t b) {
+  uint32_t u = static_cast<uint32_t>(b) << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+// c10::BFloat16 round_to_nearest_even (c10/util/BFloat16.h)
+inline uint16_t f32_to_bf16(float f) {
+  if (std::isnan(f)) return 0x7FC0;
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += ((u >> 16) & 1u) + 0x7FFFu;
+  return static_cast<uint16_t>(u >> 16);
+}
+
+inline float load_val(int dtype, const void* p, int64_t i) {
+  return dtype == DT_BF16 ? bf16_to_f32(static_cast<const uint16_t*>(p)[i])
+                          : static_cast<const float*>(p)[i];
+}
+
+// Round an fp32 result to the storage dtype and back (what a bf16 tensor op does).
+inline float round_dtype(int dtype, float f) {
+  return dtype == DT_BF16 ? bf16_to_f32(f32_to_bf16(f)) : f;
+}
+
+inline void store_val(int dtype, void* p, int64_t i, float f) {
+  if (dtype == DT_BF16)
+    static_cast<uint16_t*>(p)[i] = f32_to_bf16(f);
+  else
+    static_cast<float*>(p)[i] = f;
+}
+
+typedef std::pair<float, int64_t> elem_t;
+
+struct CompAsc {  // aten/src/ATen/native/SortingUtils.h KeyValueCompAsc
+  bool operator()(const elem_t& a, const elem_t& b) const {
+    return (!std::isnan(a.first) && std::isnan(b.first)) || (a.first < b.first);
+  }
+};
+struct CompDesc {  // KeyValueCompDesc
+  bool operator()(const elem_t& a, const elem_t& b) const {
+    return (std::isnan(a.first) && !std::isnan(b.first)) || (a.first > b.first);
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
+int orc_version(void) { return 1; }
+
+// torch.norm(x, p=2, dim=-1) on rows of length D (row_stride in elements).
+int orc_row_norms(int dtype, const void* x, int64_t rows, int64_t D, int64_t row_stride,
+                  void* out) {
+  if (D % 8 != 0) return -1;
+  for (int64_t r = 0; r < rows; ++r) {
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int64_t base = r * row_stride;
+    for (int64_t d = 0; d < D; d += 8)
+      for (int j = 0; j < 8; ++j) {
+        const float v = load_val(dtype, x, base + d + j);
+        acc[j] = std::fma(v, v, acc[j]);
+      }
+    float s = acc[0];
+    for (int j = 1; j < 8; ++j) s = s + acc[j];
+    store_val(dtype, out, r, std::sqrt(s));
+  }
+  return 0;
+}
+
+// First k entries of x.argsort(dim=-1, descending=desc) (stable=False) for one row.
+int orc_sort_prefix(int dtype, const void* vals, int64_t n, int64_t k, int desc, int64_t* out) {
+  if (k < 0 || k > n) return -1;
+  std::vector<elem_t> q(n);
+  for (int64_t i = 0; i < n; ++i) q[i] = elem_t(load_val(dtype, vals, i), i);
+  if (desc)
+    std::sort(q.begin(), q.end(), CompDesc());
+  else
+    std::sort(q.begin(), q.end(), CompAsc());
+  for (int64_t i = 0; i < k; ++i) out[i] = q[i].second;
+  return 0;
+}
+
+// Indices returned by torch.topk(x, k, dim=-1, largest, sorted=True) for one row
+// (aten/src/ATen/native/TopKImpl.h topk_impl_loop).
+int orc_topk(int dtype, const void* vals, int64_t n, int64_t k, int largest, int64_t* out) {
+  if (k < 0 || k > n) return -1;
+  if (k == 0) return 0;
+  std::vector<elem_t> q(n);
+  for (int64_t i = 0; i < n; ++i) q[i] = elem_t(load_val(dtype, vals, i), i);
+  const bool use_partial_sort = k * 64 <= n;
+  if (use_partial_sort) {
+    if (largest)
+      std::partial_sort(q.begin(), q.begin() + k, q.end(), CompDesc());
+    else
+      std::partial_sort(q.begin(), q.begin() + k, q.end(), CompAsc());
+  } else {
+    if (largest) {
+      std::nth_element(q.begin(), q.begin() + k - 1, q.end(), CompDesc());
+      std::sort(q.begin(), q.begin() + k - 1, CompDesc());
+    } else {
+      std::nth_element(q.begin(), q.begin() + k - 1, q.end(), CompAsc());
+      std::sort(q.begin(), q.begin() + k - 1, CompAsc());
+    }
+  }
+  for (int64_t i = 0; i < k; ++i) out[i] = q[i].second;
+  return 0;
+}
+
+// snapkv_lite importance scores for one (b,h) row of prefix norms (dtype values):
+//   max_norm = norms.max() + 1e-6 ; scores = max_norm - norms ; optional avg_pool1d.
+// pool_k <= 1 (or n < pool_k) means no pooling (snapkv_lite.py:104).
+int orc_snapkv_scores(int dtype, const void* norms, int64_t n, int64_t pool_k, void* out) {
+  if (n <= 0) return 0;
+  // torch.max propagates NaN
+  float mx = load_val(dtype, norms, 0);
+  bool has_nan = std::isnan(mx);
+  for (int64_t i = 1; i < n; ++i) {
+    const float v = load_val(dtype, norms, i);
+    if (std::isnan(v)) has_nan = true;
+    if (v > mx) mx = v;
+  }
+  if (has_nan) mx = NAN;
+  const float m = round_dtype(dtype, mx + static_cast<float>(1e-6));
+  std::vector<float> s(n);
+  for (int64_t i = 0; i < n; ++i) s[i] = round_dtype(dtype, m - load_val(dtype, norms, i));
+  if (pool_k > 1 && n >= pool_k) {
+    // avg_pool1d(kernel=pool_k, stride=1, padding=pool_k//2), count_include_pad=True,
+    // ceil_mode=False; output truncated to n (snapkv_lite.py:118-119).
+    const int64_t pad = pool_k / 2;
+    const int64_t out_len = n + 2 * pad - pool_k + 1;
+    const int64_t m_out = std::min(out_len, n);
+    for (int64_t i = 0; i < m_out; ++i) {
+      int64_t hs = i - pad;
+      int64_t he = std::min(hs + pool_k, n + pad);
+      const int64_t pool_size = he - hs;
+      hs = std::max<int64_t>(hs, 0);
+      he = std::min(he, n);
+      float sum = 0.0f;
+      for (int64_t j = hs; j < he; ++j) sum += s[j];
+      store_val(dtype, out, i, sum / static_cast<float>(pool_size));
+    }
+    // (out_len >= n always holds for odd and even pool_k with pad = pool_k//2)
+  } else {
+    for (int64_t i = 0; i < n; ++i) store_val(dtype, out, i, s[i]);
+  }
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,266 @@
+"""Generate golden fixtures by running the UNMODIFIED reference kvcompress (build container only).
+
+    cd /root/repo && PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 \
+        python tests/golden/gen_goldens.py
+
+The reference is imported from /root/reference (read-only); nothing of it is copied.  Outputs
+(data only) go to tests/golden/:
+  cases.json     - per case: method, kwargs, input recipe (seeds/shapes/dtype/variant), and per
+                   layer the output kind (same/view/new), shapes and SHA-256 of K_out/V_out bytes
+  positions.npz  - per case/layer: source sequence position of every output row [B,H,n_out],
+                   recovered by re-running the reference with position-encoding values
+  prims.json / prims.npz - torch.norm / argsort / topk outputs on tie-heavy rows
+Inputs are regenerated from tests/golden/prng.py recipes (hashes stored to detect drift).
+"""
+import hashlib
+import json
+import os
+import sys
+import traceback
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import prng  # noqa: E402
+
+assert os.path.abspath(os.environ.get("PYTHONPATH", "").split(":")[0]) == "/root/reference", \
+    "run with PYTHONPATH=/root/reference"
+import kvcompress  # noqa: E402  (the reference)
+from kvcompress.methods import get_compress_fn, list_methods  # noqa: E402
+
+torch.set_num_threads(8)
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def to_torch(a, dtype):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    return t.view(torch.bfloat16) if dtype == "bf16" else t
+
+
+def to_np(t, dtype):
+    t = t.contiguous()
+    return t.view(torch.int16).numpy().view(np.uint16) if dtype == "bf16" else t.numpy()
+
+
+def make_layers(case, values="data"):
+    out = []
+    for L in case["layers"]:
+        shape = tuple(L["shape"])
+        K = prng.gen_keys(L["kseed"], shape, case["dtype"], L.get("variant", "normal"))
+        if values == "data":
+            V = prng.gen_values(L["kseed"], shape, case["dtype"])
+        else:
+            V = prng.encode_positions(shape, case["dtype"])
+        out.append((K, V))
+    return out
+
+
+def kind_of(tin, tout):
+    if tout is tin:
+        return "same"
+    if tout.untyped_storage().data_ptr() == tin.untyped_storage().data_ptr():
+        return "view"
+    return "new"
+
+
+CASES = []
+
+
+def add(method, kwargs, dtype, layers, tag=""):
+    cid = f"{len(CASES):03d}_{method}_{dtype}{('_' + tag) if tag else ''}"
+    CASES.append({"id": cid, "method": method, "kwargs": kwargs, "dtype": dtype,
+                  "layers": layers})
+
+
+def L(shape, seed, variant="normal"):
+    return {"shape": list(shape), "kseed": seed, "variant": variant}
+
+
+def build_cases():
+    s = 1000
+    # ---- fix_size_l2 (BASELINE cfg2 + headline geometry, and edges) ----
+    add("fix_size_l2", {"fix_kv_size": 512, "keep_ratio": 0.0, "strategy": "keep_low",
+                        "skip_layers": []}, "bf16", [L((1, 32, 4096, 128), s + 1)], "cfg2")
+    add("fix_size_l2", {"fix_kv_size": 512, "keep_ratio": 0.0, "strategy": "keep_low",
+                        "skip_layers": []}, "bf16", [L((1, 32, 16384, 128), s + 2)], "headline")
+    for dt in ("bf16", "fp32"):
+        for D in (64, 80, 128):
+            for var in ("normal", "scaled", "few", "special"):
+                add("fix_size_l2", {"fix_kv_size": 256, "keep_ratio": 0.5, "strategy": "keep_low"},
+                    dt, [L((1, 4, 700, D), s + 10 + D), L((1, 4, 900, D), s + 11 + D),
+                         L((2, 3, 1500, D), s + 12 + D, var)], f"D{D}_{var}")
+        add("fix_size_l2", {"fix_kv_size": 300, "keep_ratio": 0.0, "strategy": "keep_high",
+                            "skip_layers": [1]}, dt,
+            [L((1, 4, 1000, 128), s + 20), L((1, 4, 1000, 128), s + 21),
+             L((1, 4, 2000, 128), s + 22, "few")], "keep_high")
+        add("fix_size_l2", {"fix_kv_size": 64, "keep_ratio": 0.3, "strategy": "keep_low",
+                            "skip_layers": []}, dt,
+            [L((1, 2, 5000, 64), s + 23, "equal"), L((1, 2, 65, 64), s + 24),
+             L((1, 2, 64, 64), s + 25)], "equal_edge")
+    add("fix_size_l2", {"fix_kv_size": 100, "keep_ratio": 1.0, "skip_layers": []}, "bf16",
+        [L((1, 2, 300, 64), s + 30)], "keep_le0_view")
+    add("fix_size_l2", {"fix_kv_size": 0, "keep_ratio": 0.5, "skip_layers": []}, "bf16",
+        [L((1, 2, 40, 64), s + 31)], "fix0_quirk")
+    add("fix_size_l2", {"fix_kv_size": 32, "strategy": "bogus", "skip_layers": []}, "bf16",
+        [L((1, 2, 40, 64), s + 32)], "bad_strategy")
+    # ---- l2_compress ----
+    for dt in ("bf16", "fp32"):
+        add("l2_compress", {"keep_ratio": 0.8, "prune_after": 100}, dt,
+            [L((1, 4, 1000, 128), s + 40), L((1, 4, 1000, 128), s + 41),
+             L((1, 4, 1000, 128), s + 42, "special"), L((1, 4, 90, 128), s + 43)], "cfg1")
+        add("l2_compress", {"keep_ratio": 0.3, "prune_after": 10, "skip_layers": []}, dt,
+            [L((2, 2, 777, 80), s + 44, "few")], "kr03")
+    add("l2_compress", {"keep_ratio": 1.0}, "bf16", [L((1, 2, 2000, 64), s + 45)], "passthrough")
+    add("l2_compress", {"keep_ratio": 0.0, "prune_after": 10, "skip_layers": []}, "bf16",
+        [L((1, 2, 50, 64), s + 46)], "kr0_empty")
+    add("l2_compress", {"keep_ratio": 0.8, "prune_after": 100, "skip_layers": []}, "bf16",
+        [L((1, 32, 16384, 128), s + 47)], "S16384")
+    # ---- streaming_llm ----
+    for dt in ("bf16", "fp32"):
+        add("streaming_llm", {"start_size": 4, "recent_size": 1020}, dt,
+            [L((1, 4, 2048, 128), s + 50), L((1, 4, 1000, 128), s + 51)], "cfg3")
+    add("streaming_llm", {"start_size": 4, "recent_size": 0, "skip_layers": [1]}, "bf16",
+        [L((1, 2, 30, 64), s + 52), L((1, 2, 30, 64), s + 53)], "recent0_quirk")
+    # ---- h2o_l2 ----
+    for dt in ("bf16", "fp32"):
+        for D in (64, 80, 128):
+            add("h2o_l2", {"start_size": 4, "heavy_hitter_size": 64, "recent_size": 444}, dt,
+                [L((1, 4, 2048, D), s + 60 + D), L((1, 4, 600, D), s + 61 + D, "few"),
+                 L((1, 4, 513, D), s + 62 + D)], f"cfg4_D{D}")
+    add("h2o_l2", {"start_size": 4, "heavy_hitter_size": 64, "recent_size": 444}, "bf16",
+        [L((1, 32, 16384, 128), s + 63)], "S16384")
+    add("h2o_l2", {"start_size": 4, "heavy_hitter_size": 64, "recent_size": 0}, "bf16",
+        [L((1, 2, 100, 64), s + 64)], "recent0_quirk")
+    add("h2o_l2", {"start_size": 2, "heavy_hitter_size": 30, "recent_size": 10}, "bf16",
+        [L((1, 2, 300, 64), s + 65, "equal"), L((1, 2, 300, 64), s + 66, "special")], "ties")
+    # ---- snapkv_lite ----
+    for dt in ("bf16", "fp32"):
+        for var in ("normal", "few", "tiny", "zero", "special"):
+            add("snapkv_lite", {"observation_window": 32, "keep_size": 512, "pooling_kernel": 5},
+                dt, [L((1, 4, 2048, 128), s + 70), L((1, 4, 1500, 80), s + 71, var)],
+                f"cfg5_{var}")
+        add("snapkv_lite", {"observation_window": 8, "keep_size": 40, "pooling_kernel": 4}, dt,
+            [L((1, 4, 4096, 64), s + 72), L((1, 2, 2048, 64), s + 73, "few")], "partialsort_even")
+        add("snapkv_lite", {"observation_window": 16, "keep_size": 100, "pooling_kernel": 1}, dt,
+            [L((1, 4, 600, 64), s + 74)], "nopool")
+    add("snapkv_lite", {"observation_window": 0, "keep_size": 50, "pooling_kernel": 5}, "bf16",
+        [L((1, 2, 120, 64), s + 75)], "obs0_quirk")
+    add("snapkv_lite", {"observation_window": 60, "keep_size": 50, "pooling_kernel": 5}, "bf16",
+        [L((1, 2, 120, 64), s + 76), L((1, 2, 55, 64), s + 77)], "keep_le_obs")
+    add("snapkv_lite", {"observation_window": 32, "keep_size": 512, "pooling_kernel": 7}, "bf16",
+        [L((1, 32, 16384, 128), s + 78)], "S16384")
+    # ---- pyramid_kv ----
+    for dt in ("bf16", "fp32"):
+        add("pyramid_kv", {"base_size": 512, "layer_decay": 0.9}, dt,
+            [L((1, 4, 1024, 128), s + 80 + j) for j in range(6)], "cfg5")
+    add("pyramid_kv", {"base_size": 300, "min_size": 40, "profile": "linear"}, "bf16",
+        [L((1, 2, 400, 64), s + 90 + j) for j in range(5)], "linear")
+    add("pyramid_kv", {"base_size": 200, "profile": "constant", "skip_layers": [0]}, "bf16",
+        [L((1, 2, 400, 64), s + 96 + j) for j in range(3)], "constant")
+    add("pyramid_kv", {"base_size": 16, "min_size": 1, "layer_decay": 0.5}, "bf16",
+        [L((1, 2, 40, 64), s + 100 + j) for j in range(6)], "tiny_sizes")
+    # ---- adaptive_l2 ----
+    for dt in ("bf16", "fp32"):
+        add("adaptive_l2", {"target_size": 512}, dt,
+            [L((1, 4, 2048, 128), s + 110), L((1, 4, 600, 128), s + 111),
+             L((1, 4, 1024, 128), s + 112, "few"), L((1, 4, 200, 128), s + 113)], "mixed")
+    add("adaptive_l2", {"target_size": 6, "soft_limit": 2, "hard_limit": 64}, "bf16",
+        [L((1, 2, 100, 64), s + 114), L((1, 2, 3, 64), s + 115), L((1, 2, 30, 64), s + 116)],
+        "edges")
+    add("adaptive_l2", {"target_size": 512}, "bf16", [L((1, 32, 16384, 128), s + 117)], "S16384")
+    # ---- recent_only ----
+    add("recent_only", {"window_size": 512}, "bf16",
+        [L((1, 2, 1024, 64), s + 120), L((1, 2, 1024, 64), s + 121),
+         L((1, 2, 1024, 64), s + 122), L((1, 2, 300, 64), s + 123)], "default")
+
+
+def run_case(case, positions):
+    fn = get_compress_fn(case["method"])
+    dt = case["dtype"]
+    rec = dict(case)
+    layers = make_layers(case)
+    rec["input_sha"] = [sha(K) for K, _ in layers]
+    tin = [(to_torch(K, dt), to_torch(V, dt)) for K, V in layers]
+    try:
+        out = fn(list(tin), **case["kwargs"])
+    except Exception as e:  # reference raises -> record the exception type
+        rec["error"] = type(e).__name__
+        rec["out"] = None
+        return rec
+    rec["error"] = None
+    enc = [(to_torch(K, dt), to_torch(prng.encode_positions(K.shape, dt), dt)) for K, _ in layers]
+    out_enc = fn(list(enc), **case["kwargs"])
+    res = []
+    for li, ((ki, vi), (ko, vo), (_, veo)) in enumerate(zip(tin, out, out_enc)):
+        kk, kv = kind_of(ki, ko), kind_of(vi, vo)
+        assert kk == kv
+        r = {"kind": kk, "k_shape": list(ko.shape), "v_shape": list(vo.shape),
+             "k_sha": sha(to_np(ko, dt)), "v_sha": sha(to_np(vo, dt))}
+        if kk != "same":
+            pos, ok = prng.decode_positions(to_np(veo, dt), dt)
+            assert ok, case["id"]
+            key = f"{case['id']}__L{li}"
+            positions[key] = pos.astype(np.int16 if ko.shape[2] and pos.max() < 32768 else np.int32)
+            r["pos_key"] = key
+        res.append(r)
+    rec["out"] = res
+    return rec
+
+
+def gen_prims():
+    """Direct fixtures for the torch primitives the oracle restates."""
+    meta, arrs = [], {}
+    for dt in ("bf16", "fp32"):
+        for D in (64, 80, 128):
+            for var in ("normal", "scaled", "special", "few"):
+                seed = 5000 + D + (0 if dt == "bf16" else 7) + 11 * ("normal", "scaled", "special", "few").index(var)
+                K = prng.gen_keys(seed, (1, 4, 2048, D), dt, var)
+                n = torch.norm(to_torch(K, dt), p=2, dim=-1)
+                nn = to_np(n, dt)
+                key = f"norm_{dt}_D{D}_{var}"
+                arrs[key] = nn
+                asc = n.argsort(dim=-1).numpy().astype(np.int16)
+                desc = n.argsort(dim=-1, descending=True).numpy().astype(np.int16)
+                arrs[key + "_argsort"] = asc
+                arrs[key + "_argsort_desc"] = desc
+                tk = {}
+                for k in (1, 16, 31, 32, 480, 2047):
+                    tk[k] = torch.topk(n, k, dim=-1)[1].numpy().astype(np.int16)
+                    arrs[f"{key}_topk{k}"] = tk[k]
+                meta.append({"key": key, "dtype": dt, "D": D, "variant": var, "seed": seed,
+                             "shape": [1, 4, 2048, D], "input_sha": sha(K),
+                             "topk_ks": [1, 16, 31, 32, 480, 2047]})
+    return meta, arrs
+
+
+def main():
+    build_cases()
+    positions = {}
+    recs = []
+    for c in CASES:
+        try:
+            recs.append(run_case(c, positions))
+        except Exception:
+            traceback.print_exc()
+            raise
+        print(c["id"], "error" if recs[-1]["error"] else "ok", flush=True)
+    meta = {"torch": torch.__version__, "cpu_capability": torch.backends.cpu.get_cpu_capability(),
+            "reference_version": kvcompress.__version__, "list_methods": list_methods(),
+            "generator": "tests/golden/gen_goldens.py"}
+    with open(os.path.join(HERE, "cases.json"), "w") as f:
+        json.dump({"meta": meta, "cases": recs}, f, indent=1)
+    np.savez_compressed(os.path.join(HERE, "positions.npz"), **positions)
+    pm, pa = gen_prims()
+    with open(os.path.join(HERE, "prims.json"), "w") as f:
+        json.dump({"meta": meta, "prims": pm}, f, indent=1)
+    np.savez_compressed(os.path.join(HERE, "prims.npz"), **pa)
+    print("wrote", len(recs), "cases,", len(positions), "position arrays,", len(pm), "prim sets")
+
+
+if __name__ == "__main__":
+    main()
