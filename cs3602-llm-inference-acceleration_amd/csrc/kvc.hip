@@ -1,0 +1,741 @@
+// kvc.hip -- MI355X (gfx950) kernels and C ABI of the KV-cache compression engine.
+// ABI documentation: include/kvc.h.  Design and rooflines: DESIGN.md.
+//
+// Kernels (one launch each, all layers of a compress_fn call batched into every launch):
+//   score_kernel  : HBM-streaming key L2 norms.  One wave = one 64-token tile of one (b,h) row;
+//                   tiles are read with coalesced 16-B loads, transposed through a padded LDS
+//                   slab so each lane owns one token row, and reduced with torch.norm's exact
+//                   8-accumulator FMA order (reference: torch.norm at fix_size_l2.py:106 etc.).
+//   select_kernel : one 1024-thread workgroup per (layer, b, h) row, the row's keys resident in
+//                   LDS.  Reproduces the first-k SET of libstdc++ std::sort (argsort, stable=False)
+//                   or std::nth_element / std::partial_sort (torch.topk) by following only the
+//                   chain of Hoare partitions that straddle position k; each partition is computed
+//                   in parallel from ballot prefix ranks ("Selection").  Emits the
+//                   kept zone-local indices in ascending order (= torch.sort(indices) of the
+//                   reference, e.g. fix_size_l2.py:129).
+//   gather_kernel : segment copy sink ++ zone[selected] ++ tail for K and V (torch.gather +
+//                   torch.cat of the reference, e.g. fix_size_l2.py:137-147).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "kvc.h"
+#include "kvc_common.h"
+#include "kvc_serial.h"
+
+namespace kvc {
+
+constexpr int kTile = 64;  // tokens per score tile (one per lane)
+constexpr int kScoreThreads = 256;
+constexpr int kScoreWaves = kScoreThreads / 64;
+constexpr int kSelThreads = 1024;
+constexpr int kSelWaves = kSelThreads / 64;
+constexpr int kZoneMax = 16384;  // longest zone whose keys fit the select kernel's LDS
+constexpr int kGatherThreads = 256;
+constexpr int kBig = 0x7FFFFFFF;
+
+template <int DT>
+struct DTypeTraits;
+template <>
+struct DTypeTraits<KVC_BF16> {
+  static constexpr int esz = 2;
+  typedef uint16_t key_t;
+};
+template <>
+struct DTypeTraits<KVC_F32> {
+  static constexpr int esz = 4;
+  typedef uint32_t key_t;
+};
+
+template <int DT>
+__device__ __forceinline__ float load_dt(const char* base, int i) {
+  if constexpr (DT == KVC_BF16)
+    return bf16_to_f32(reinterpret_cast<const uint16_t*>(base)[i]);
+  else
+    return reinterpret_cast<const float*>(base)[i];
+}
+
+template <int DT>
+__device__ __forceinline__ float round_dt(float f) {
+  if constexpr (DT == KVC_BF16)
+    return bf16_to_f32(f32_to_bf16_rne(f));
+  else
+    return f;
+}
+
+template <int DT>
+__device__ __forceinline__ typename DTypeTraits<DT>::key_t key_of(float f, bool desc) {
+  if constexpr (DT == KVC_BF16)
+    return key_bf16(f32_to_bf16_rne(f), desc);
+  else
+    return key_f32(f32_to_bits(f), desc);
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---------------------------------------------------------------------------------------------
+// SCORE
+// ---------------------------------------------------------------------------------------------
+template <int DT, int NC>
+__device__ __forceinline__ void accum_chunk(float (&acc)[8], const uint4 x, int gchunk) {
+  if constexpr (DT == KVC_BF16) {
+    // chunk c holds elements 8c..8c+7: element e feeds accumulator e
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float e0 = bits_to_f32(w[q] << 16);
+      const float e1 = bits_to_f32(w[q] & 0xFFFF0000u);
+      acc[2 * q] = __builtin_fmaf(e0, e0, acc[2 * q]);
+      acc[2 * q + 1] = __builtin_fmaf(e1, e1, acc[2 * q + 1]);
+    }
+  } else {
+    // chunk c holds elements 4c..4c+3: accumulators 4*(c&1) + e
+    const int j0 = (gchunk & 1) * 4;
+    const float e[4] = {bits_to_f32(x.x), bits_to_f32(x.y), bits_to_f32(x.z), bits_to_f32(x.w)};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[j0 + q] = __builtin_fmaf(e[q], e[q], acc[j0 + q]);
+  }
+}
+
+template <int DT, int NC>
+__global__ void __launch_bounds__(kScoreThreads)
+    score_kernel(const kvc_layer_t* __restrict__ L, int nl, int H, int64_t total_tiles,
+                 char* __restrict__ norms, int64_t norm_stride) {
+  constexpr int ESZ = DTypeTraits<DT>::esz;
+  constexpr int CP = (NC % 8 == 0) ? 8 : 10;  // 16-B chunks per token per phase
+  constexpr int NPH = NC / CP;
+  constexpr int ROWB = CP * 16 + 16;  // padded LDS row: conflict-free ds_read_b128 per lane
+  __shared__ __attribute__((aligned(16))) char lds[kScoreWaves][kTile * ROWB];
+
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t g = (int64_t)blockIdx.x * kScoreWaves + wid;
+  if (g >= total_tiles) return;
+
+  int lo = 0, hi = nl - 1;  // largest layer with tile0 <= g
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (L[mid].tile0 <= g)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  const kvc_layer_t* ly = L + lo;
+  const int zlen = ly->zone_len;
+  const int tpr = (zlen + kTile - 1) / kTile;
+  const int local = (int)(g - ly->tile0);
+  const int row = local / tpr;
+  const int tt = local - row * tpr;
+  const int b = row / H, h = row - (row / H) * H;
+  const int tok0 = tt * kTile;
+  const int ntok = min(kTile, zlen - tok0);
+  const int64_t sbytes = ly->k_stride[2] * ESZ;
+  const char* base = static_cast<const char*>(ly->k) +
+                     ((int64_t)b * ly->k_stride[0] + (int64_t)h * ly->k_stride[1] +
+                      (int64_t)(ly->zone_start + tok0) * ly->k_stride[2]) * ESZ;
+  char* wl = lds[wid];
+
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ph = 0; ph < NPH; ++ph) {
+    uint4 v[CP];
+#pragma unroll
+    for (int it = 0; it < CP; ++it) {
+      const int q = it * 64 + lane;
+      const int tok = q / CP, c = q - (q / CP) * CP;
+      if (tok < ntok)
+        v[it] = *reinterpret_cast<const uint4*>(base + tok * sbytes + (ph * CP + c) * 16);
+      else
+        v[it] = make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int it = 0; it < CP; ++it) {
+      const int q = it * 64 + lane;
+      const int tok = q / CP, c = q - (q / CP) * CP;
+      *reinterpret_cast<uint4*>(wl + tok * ROWB + c * 16) = v[it];
+    }
+    wave_sync();
+#pragma unroll
+    for (int c = 0; c < CP; ++c) {
+      const uint4 x = *reinterpret_cast<const uint4*>(wl + lane * ROWB + c * 16);
+      accum_chunk<DT, NC>(acc, x, ph * CP + c);
+    }
+    wave_sync();
+  }
+  if (lane < ntok) {
+    float s = acc[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) s = s + acc[j];
+    const float r = __builtin_sqrtf(s);
+    char* nrow = norms + (int64_t)(ly->row0 + row) * norm_stride * ESZ;
+    if constexpr (DT == KVC_BF16)
+      reinterpret_cast<uint16_t*>(nrow)[tok0 + lane] = (uint16_t)f32_to_bf16_rne(r);
+    else
+      reinterpret_cast<float*>(nrow)[tok0 + lane] = r;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// SELECT
+// ---------------------------------------------------------------------------------------------
+template <typename KeyT>
+struct SelScalars {
+  int lo, hi, state, m, gnext;
+  KeyT p;
+  int wa[kSelWaves];
+  int wb[kSelWaves];
+  float fmax[kSelWaves];
+  int fnan[kSelWaves];
+};
+
+__device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
+__device__ __forceinline__ uint64_t lanemask_le(int lane) {
+  return lane == 63 ? ~0ull : ((1ull << (lane + 1)) - 1ull);
+}
+
+// snapkv_lite importance scores (snapkv_lite.py:96-121) computed from the row's norms and
+// written as sort keys:  m = dt(max(norms) + 1e-6);  s = dt(m - norm);
+// pooled_i = dt(sum_{window} s / pool_size) (avg_pool1d, zero pad, count_include_pad).
+template <int DT, typename KeyT>
+__device__ void snapkv_keys(const char* nrow, int n, int pool_k, bool desc, KeyT* key,
+                            char* tmp, SelScalars<KeyT>& sc) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  float mx = -__builtin_huge_valf();
+  int has_nan = 0;
+  for (int i = tid; i < n; i += kSelThreads) {
+    const float v = load_dt<DT>(nrow, i);
+    if (v != v) has_nan = 1;
+    else if (v > mx) mx = v;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float y = __shfl_xor(mx, o, 64);
+    mx = y > mx ? y : mx;
+    has_nan |= __shfl_xor(has_nan, o, 64);
+  }
+  if (lane == 0) {
+    sc.fmax[wid] = mx;
+    sc.fnan[wid] = has_nan;
+  }
+  __syncthreads();
+  mx = sc.fmax[0];
+  has_nan = sc.fnan[0];
+  for (int w = 1; w < kSelWaves; ++w) {
+    mx = sc.fmax[w] > mx ? sc.fmax[w] : mx;
+    has_nan |= sc.fnan[w];
+  }
+  if (has_nan) mx = __builtin_nanf("");
+  const float m = round_dt<DT>(mx + 1e-6f);
+  for (int i = tid; i < n; i += kSelThreads) {
+    const float s = round_dt<DT>(m - load_dt<DT>(nrow, i));
+    if constexpr (DT == KVC_BF16)
+      reinterpret_cast<uint16_t*>(tmp)[i] = (uint16_t)f32_to_bf16_rne(s);
+    else
+      reinterpret_cast<float*>(tmp)[i] = s;
+  }
+  __syncthreads();
+  const bool pool = pool_k > 1 && n >= pool_k;
+  const int pad = pool_k / 2;
+  for (int i = tid; i < n; i += kSelThreads) {
+    float r;
+    if (pool) {
+      int hs = i - pad;
+      int he = min(hs + pool_k, n + pad);
+      const int psize = he - hs;
+      hs = max(hs, 0);
+      he = min(he, n);
+      float sum = 0.f;
+      for (int j = hs; j < he; ++j) sum = sum + load_dt<DT>(tmp, j);
+      r = sum / (float)psize;
+    } else {
+      r = load_dt<DT>(tmp, i);
+    }
+    key[i] = key_of<DT>(r, desc);
+  }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(kSelThreads)
+    select_kernel(const kvc_layer_t* __restrict__ L, int BH, int order, int algo,
+                  const char* __restrict__ norms, int64_t norm_stride,
+                  int32_t* __restrict__ out_idx, int64_t idx_stride) {
+  typedef typename DTypeTraits<DT>::key_t KeyT;
+  constexpr int ESZ = DTypeTraits<DT>::esz;
+  // LDS: key[kZoneMax] | idx[kZoneMax] (u16) | spos[kZoneMax + 8] (u16) | scalars
+  constexpr int KEY_B = kZoneMax * (int)sizeof(KeyT);
+  constexpr int IDX_B = kZoneMax * 2;
+  constexpr int SPOS_B = (kZoneMax + 8) * 2;
+  __shared__ __attribute__((aligned(16))) char smem[KEY_B + IDX_B + SPOS_B];
+  __shared__ SelScalars<KeyT> sc;
+  KeyT* key = reinterpret_cast<KeyT*>(smem);
+  uint16_t* idx = reinterpret_cast<uint16_t*>(smem + KEY_B);
+  uint16_t* spos = reinterpret_cast<uint16_t*>(smem + KEY_B + IDX_B);
+
+  const int row = blockIdx.x;
+  const kvc_layer_t* ly = L + row / BH;
+  const int n = ly->zone_len;
+  const int k = ly->n_select;
+  if (k <= 0 || n <= 0 || n > kZoneMax) return;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int32_t* out = out_idx + (int64_t)row * idx_stride;
+  if (k >= n) {  // keep everything (e.g. h2o_l2 when the middle is no longer than heavy_hitter)
+    for (int i = tid; i < n; i += kSelThreads) out[i] = i;
+    return;
+  }
+  const bool desc = order == KVC_DESC;
+  const char* nrow = norms + (int64_t)row * norm_stride * ESZ;
+
+  // ---- keys ----
+  if (ly->score_mode == KVC_SCORE_SNAPKV) {
+    // scratch for the unpooled scores: bf16 -> spos region, fp32 -> idx+spos (64 KiB + 16 B)
+    char* tmp = (DT == KVC_BF16) ? reinterpret_cast<char*>(spos) : reinterpret_cast<char*>(idx);
+    snapkv_keys<DT, KeyT>(nrow, n, ly->pool_kernel, desc, key, tmp, sc);
+    __syncthreads();
+    for (int i = tid; i < n; i += kSelThreads) idx[i] = (uint16_t)i;
+  } else {
+    for (int i = tid; i < n; i += kSelThreads) {
+      if constexpr (DT == KVC_BF16)
+        key[i] = key_bf16(reinterpret_cast<const uint16_t*>(nrow)[i], desc);
+      else
+        key[i] = key_f32(reinterpret_cast<const uint32_t*>(nrow)[i], desc);
+      idx[i] = (uint16_t)i;
+    }
+  }
+  __syncthreads();
+
+  // ---- reference-exact k-selection ----
+  const bool topk = algo == KVC_ALGO_TOPK;
+  const bool partial = topk && (int64_t)k * 64 <= n;  // aten TopKImpl.h: use_partial_sort
+  const int thr = topk ? 3 : 16;  // introselect / introsort segment threshold
+  int lo = 0, hi = n, depth = 2 * floor_log2(n);  // chain state, owned by thread 0
+  bool first = true;
+  while (true) {
+    if (tid == 0) {
+      int state = 1;
+      if (partial) {
+        heap_select(key, idx, k, n);  // std::partial_sort's heap select; set = first k
+      } else {
+        if (!first) {  // finish the previous partition: cut = min(g_{m+1}, s_m)
+          const int cut = min(sc.gnext, sc.m > 0 ? (int)spos[sc.m] : kBig);
+          if (topk) {  // std::__introselect: if (cut <= nth) first = cut; else last = cut;
+            if (cut <= k - 1) lo = cut; else hi = cut;
+          } else {     // std::__introsort_loop: right part recursed, loop on the left
+            if (k <= cut) hi = cut; else lo = cut;
+          }
+        }
+        if (lo == k || hi == k) {
+          // a partition boundary sits exactly at k: the first-k set is final
+        } else if (hi - lo <= thr) {
+          insertion_sort(key, idx, lo, hi);  // final insertion sort (stable) of the segment
+        } else if (depth == 0) {  // depth limit: libstdc++ switches to heap algorithms
+          if (topk) {
+            heap_select(key + lo, idx + lo, k - lo, hi - lo);
+            kv_swap(key, idx, lo, k - 1);
+          } else {
+            make_heap(key + lo, idx + lo, hi - lo);
+            sort_heap(key + lo, idx + lo, hi - lo);
+          }
+        } else {
+          --depth;
+          move_median_to_first(key, idx, lo, lo + 1, lo + (hi - lo) / 2, hi - 1);
+          sc.p = key[lo];
+          sc.lo = lo;
+          sc.hi = hi;
+          sc.m = 0;
+          sc.gnext = kBig;
+          state = 0;
+        }
+      }
+      sc.state = state;
+    }
+    first = false;
+    __syncthreads();
+    if (sc.state) break;
+
+    // ---- one std::__unguarded_partition(lo+1, hi, pivot=lo), computed in parallel ----
+    // g_t: t-th position (ascending) in [lo+1,hi) with !(key < p); s_t: t-th position
+    // (descending) with !(p < key), followed by the pivot slot lo.  libstdc++ swaps g_t<->s_t
+    // for every t with g_t < s_t (a prefix of t) and returns min(g_{m+1}, s_m).
+    const int plo = sc.lo, phi = sc.hi;
+    const KeyT p = sc.p;
+    const int m1 = phi - plo - 1;
+    const int J = (m1 + kSelThreads - 1) / kSelThreads;  // <= 16 positions per lane
+    const int wbeg = plo + 1 + wid * J * 64;
+    uint32_t gem = 0, lem = 0;
+    int cge = 0, cle = 0;
+    for (int j = 0; j < J; ++j) {
+      const int pos = wbeg + j * 64 + lane;
+      const bool valid = pos < phi;
+      const KeyT kk = valid ? key[pos] : (KeyT)0;
+      const bool ge = valid && !(kk < p);
+      const bool le = valid && !(p < kk);
+      gem |= (uint32_t)ge << j;
+      lem |= (uint32_t)le << j;
+      cge += __popcll(__ballot(ge));
+      cle += __popcll(__ballot(le));
+    }
+    if (lane == 0) {
+      sc.wa[wid] = cge;
+      sc.wb[wid] = cle;
+    }
+    __syncthreads();
+    int ge_before = 0, le_before = 0, tot_le = 0;
+    for (int w = 0; w < kSelWaves; ++w) {
+      const int a = sc.wa[w], bb = sc.wb[w];
+      if (w < wid) {
+        ge_before += a;
+        le_before += bb;
+      }
+      tot_le += bb;
+    }
+    {  // s positions by descending rank (1-based); the pivot slot closes the list
+      int run = le_before;
+      for (int j = 0; j < J; ++j) {
+        const bool le = (lem >> j) & 1u;
+        const uint64_t bl = __ballot(le);
+        if (le) {
+          const int incl = run + __popcll(bl & lanemask_le(lane));
+          spos[tot_le - incl + 1] = (uint16_t)(wbeg + j * 64 + lane);
+        }
+        run += __popcll(bl);
+      }
+      if (tid == 0) spos[tot_le + 1] = (uint16_t)plo;
+    }
+    __syncthreads();
+    {  // number of swaps m = #{t : g_t < s_t}
+      int run = ge_before, cnt = 0;
+      for (int j = 0; j < J; ++j) {
+        const bool ge = (gem >> j) & 1u;
+        const uint64_t bg = __ballot(ge);
+        if (ge) {
+          const int t = run + __popcll(bg & lanemask_lt(lane)) + 1;
+          if (t <= tot_le + 1 && (int)spos[t] > wbeg + j * 64 + lane) ++cnt;
+        }
+        run += __popcll(bg);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+      if (lane == 0 && cnt) atomicAdd(&sc.m, cnt);
+    }
+    __syncthreads();
+    {  // the swaps (all pairs are disjoint) and g_{m+1}
+      const int msw = sc.m;
+      int run = ge_before;
+      for (int j = 0; j < J; ++j) {
+        const bool ge = (gem >> j) & 1u;
+        const uint64_t bg = __ballot(ge);
+        if (ge) {
+          const int t = run + __popcll(bg & lanemask_lt(lane)) + 1;
+          const int pos = wbeg + j * 64 + lane;
+          if (t <= msw)
+            kv_swap(key, idx, pos, (int)spos[t]);
+          else if (t == msw + 1)
+            sc.gnext = pos;
+        }
+        run += __popcll(bg);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- emit the kept set {idx[0..k)} as ascending zone-local indices ----
+  uint16_t* flag = spos;
+  for (int i = tid; i < n; i += kSelThreads) flag[i] = 0;
+  __syncthreads();
+  for (int i = tid; i < k; i += kSelThreads) flag[idx[i]] = 1;
+  __syncthreads();
+  const int J = (n + kSelThreads - 1) / kSelThreads;
+  const int wbeg = wid * J * 64;
+  uint32_t fm = 0;
+  int c = 0;
+  for (int j = 0; j < J; ++j) {
+    const int pos = wbeg + j * 64 + lane;
+    const bool f = pos < n && flag[pos] != 0;
+    fm |= (uint32_t)f << j;
+    c += __popcll(__ballot(f));
+  }
+  if (lane == 0) sc.wa[wid] = c;
+  __syncthreads();
+  int run = 0;
+  for (int w = 0; w < wid; ++w) run += sc.wa[w];
+  for (int j = 0; j < J; ++j) {
+    const bool f = (fm >> j) & 1u;
+    const uint64_t bf = __ballot(f);
+    if (f) out[run + __popcll(bf & lanemask_lt(lane))] = wbeg + j * 64 + lane;
+    run += __popcll(bf);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// GATHER
+// ---------------------------------------------------------------------------------------------
+template <int DT, int NC>
+__global__ void __launch_bounds__(kGatherThreads)
+    gather_kernel(const kvc_layer_t* __restrict__ L, int nl, int H, int BH,
+                  const int32_t* __restrict__ gidx, int64_t idx_stride, int64_t total) {
+  constexpr int ESZ = DTypeTraits<DT>::esz;
+  for (int64_t u = (int64_t)blockIdx.x * kGatherThreads + threadIdx.x; u < total;
+       u += (int64_t)gridDim.x * kGatherThreads) {
+    int lo = 0, hi = nl - 1;  // largest layer with unit0 <= u
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (L[mid].unit0 <= u)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    const kvc_layer_t* ly = L + lo;
+    const int n_out = ly->n_out;
+    const int per_row = n_out * NC;
+    int r = (int)(u - ly->unit0);
+    const int is_v = r >= BH * per_row;
+    if (is_v) r -= BH * per_row;
+    const int row = r / per_row;
+    r -= row * per_row;
+    const int t = r / NC;
+    const int c = r - t * NC;
+    const int b = row / H, h = row - (row / H) * H;
+    int src;
+    bool gathered = false;
+    if (t < ly->sink_len) {
+      src = t;
+    } else if (t < ly->sink_len + ly->n_select) {
+      int zi = gidx[(int64_t)(ly->row0 + row) * idx_stride + (t - ly->sink_len)];
+      zi = min(max(zi, 0), ly->zone_len - 1);  // never read outside the zone, whatever the index
+      src = ly->zone_start + zi;
+      gathered = true;
+    } else {
+      src = ly->tail_start + (t - ly->sink_len - ly->n_select);
+    }
+    const int64_t* st = is_v ? ly->v_stride : ly->k_stride;
+    const char* sp = static_cast<const char*>(is_v ? ly->v : ly->k) +
+                     ((int64_t)b * st[0] + (int64_t)h * st[1] + (int64_t)src * st[2]) * ESZ +
+                     c * 16;
+    uint4 x = *reinterpret_cast<const uint4*>(sp);
+    if constexpr (DT == KVC_BF16) {
+      if (gathered) {
+        x.x = canon_nan_bf16x2(x.x);
+        x.y = canon_nan_bf16x2(x.y);
+        x.z = canon_nan_bf16x2(x.z);
+        x.w = canon_nan_bf16x2(x.w);
+      }
+    }
+    char* dp = static_cast<char*>(is_v ? ly->v_out : ly->k_out) +
+               (((int64_t)row * n_out + t) * NC + c) * 16;
+    *reinterpret_cast<uint4*>(dp) = x;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+static inline int esize(int dtype) { return dtype == KVC_BF16 ? 2 : 4; }
+static inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_plan_info_t* info,
+                     bool fill) {
+  if (!p || nl < 0 || (nl > 0 && !layers)) return KVC_E_ARG;
+  if (p->dtype != KVC_BF16 && p->dtype != KVC_F32) return KVC_E_DTYPE;
+  if (p->batch < 1 || p->heads < 1 || p->head_dim < 1) return KVC_E_ARG;
+  if (p->order != KVC_ASC && p->order != KVC_DESC) return KVC_E_ARG;
+  if (p->algo != KVC_ALGO_SORT && p->algo != KVC_ALGO_TOPK) return KVC_E_ARG;
+  const int es = esize(p->dtype);
+  const int rowb = p->head_dim * es;
+  if (rowb % 16) return KVC_E_HEADDIM;
+  const int nc = rowb / 16;
+  if (nc != 8 && nc != 10 && nc != 16 && nc != 20 && nc != 32) return KVC_E_HEADDIM;
+  const int64_t BH = (int64_t)p->batch * p->heads;
+  if (BH * nl > 0x7FFFFFFF) return KVC_E_ARG;
+  int64_t tiles = 0, units = 0, max_zone = 0, max_sel = 0;
+  for (int l = 0; l < nl; ++l) {
+    kvc_layer_t& y = layers[l];
+    const int S = y.seq_len;
+    if (S < 0 || y.zone_start < 0 || y.zone_len < 0 || (int64_t)y.zone_start + y.zone_len > S ||
+        y.n_select < 0 || y.n_select > y.zone_len || y.sink_len < 0 || y.sink_len > S ||
+        y.tail_start < 0 || y.tail_len < 0 || (int64_t)y.tail_start + y.tail_len > S ||
+        (y.score_mode != KVC_SCORE_NORM && y.score_mode != KVC_SCORE_SNAPKV))
+      return KVC_E_ARG;
+    const int64_t n_out = (int64_t)y.sink_len + y.n_select + y.tail_len;
+    if (n_out > 0x7FFFFFFF || 2 * BH * n_out * nc > 0x7FFFFFFF) return KVC_E_ARG;
+    const bool needs_select = y.n_select > 0 && y.n_select < y.zone_len;
+    if (needs_select && y.zone_len > kZoneMax) return KVC_E_TOO_LONG;
+    if (n_out > 0) {
+      if (!y.k || !y.v || !y.k_out || !y.v_out) return KVC_E_ARG;
+      if (!aligned16(y.k) || !aligned16(y.v) || !aligned16(y.k_out) || !aligned16(y.v_out))
+        return KVC_E_ALIGN;
+      const int64_t* ks = y.k_stride;
+      const int64_t* vs = y.v_stride;
+      if ((p->batch > 1 && ((ks[0] * es) % 16 || (vs[0] * es) % 16)) ||
+          (p->heads > 1 && ((ks[1] * es) % 16 || (vs[1] * es) % 16)) ||
+          (S > 1 && ((ks[2] * es) % 16 || (vs[2] * es) % 16)))
+        return KVC_E_ALIGN;
+    }
+    const int64_t tl = needs_select ? BH * ((y.zone_len + kTile - 1) / kTile) : 0;
+    const int64_t ul = 2 * BH * n_out * nc;
+    if (fill) {
+      y.n_out = (int32_t)n_out;
+      y.row0 = (int32_t)(l * BH);
+      y.tile0 = (int32_t)tiles;
+      y.unit0 = units;
+    } else if (y.n_out != n_out || y.row0 != l * BH || y.tile0 != tiles || y.unit0 != units) {
+      return KVC_E_ARG;
+    }
+    if (needs_select && y.zone_len > max_zone) max_zone = y.zone_len;
+    if (y.n_select > max_sel) max_sel = y.n_select;
+    tiles += tl;
+    units += ul;
+    if (tiles > 0x7FFFFFFF) return KVC_E_ARG;
+  }
+  if (info) {
+    const int64_t rows = BH * nl;
+    info->rows = rows;
+    info->score_tiles = tiles;
+    info->gather_units = units;
+    info->norm_row_stride = (int64_t)round_up((size_t)max_zone, kTile);
+    info->index_row_stride = (int64_t)round_up((size_t)(max_sel > 0 ? max_sel : 1), 16);
+    size_t off = 0;
+    info->desc_offset = off;
+    off = round_up(off + (size_t)nl * sizeof(kvc_layer_t), 256);
+    info->norm_offset = off;
+    off = round_up(off + (size_t)rows * info->norm_row_stride * es, 256);
+    info->index_offset = off;
+    off = round_up(off + (size_t)rows * info->index_row_stride * 4, 256);
+    info->workspace_bytes = off;
+  }
+  return KVC_OK;
+}
+
+template <int DT, int NC>
+static void launch_score(const kvc_layer_t* Ld, int nl, int H, int64_t tiles, char* norms,
+                         int64_t nstride, hipStream_t s) {
+  const unsigned grid = (unsigned)((tiles + kScoreWaves - 1) / kScoreWaves);
+  hipLaunchKernelGGL((score_kernel<DT, NC>), dim3(grid), dim3(kScoreThreads), 0, s, Ld, nl, H,
+                     tiles, norms, nstride);
+}
+
+template <int DT, int NC>
+static void launch_gather(const kvc_layer_t* Ld, int nl, int H, int BH, const int32_t* idx,
+                          int64_t istride, int64_t units, hipStream_t s) {
+  int64_t blocks = (units + kGatherThreads - 1) / kGatherThreads;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL((gather_kernel<DT, NC>), dim3((unsigned)blocks), dim3(kGatherThreads), 0, s,
+                     Ld, nl, H, BH, idx, istride, units);
+}
+
+template <int DT>
+static void dispatch_nc(int nc, bool score, const kvc_layer_t* Ld, int nl, int H, int BH,
+                        int64_t work, char* norms, int64_t nstride, const int32_t* idx,
+                        int64_t istride, hipStream_t s) {
+#define KVC_NC_CASE(NCV)                                                   \
+  case NCV:                                                                \
+    if (score)                                                             \
+      launch_score<DT, NCV>(Ld, nl, H, work, norms, nstride, s);           \
+    else                                                                   \
+      launch_gather<DT, NCV>(Ld, nl, H, BH, idx, istride, work, s);        \
+    break;
+  switch (nc) {
+    KVC_NC_CASE(8)
+    KVC_NC_CASE(10)
+    KVC_NC_CASE(16)
+    KVC_NC_CASE(20)
+    KVC_NC_CASE(32)
+    default:
+      break;
+  }
+#undef KVC_NC_CASE
+}
+
+}  // namespace kvc
+
+extern "C" {
+
+int kvc_version(void) { return KVC_ABI_VERSION; }
+size_t kvc_layer_struct_size(void) { return sizeof(kvc_layer_t); }
+int kvc_max_zone_len(void) { return kvc::kZoneMax; }
+
+const char* kvc_status_string(int s) {
+  switch (s) {
+    case KVC_OK: return "ok";
+    case KVC_E_ARG: return "invalid argument";
+    case KVC_E_DTYPE: return "unsupported dtype (bf16/fp32 only)";
+    case KVC_E_HEADDIM: return "unsupported head_dim";
+    case KVC_E_ALIGN: return "pointer or stride not 16-byte aligned";
+    case KVC_E_TOO_LONG: return "scored zone longer than kvc_max_zone_len()";
+    case KVC_E_WORKSPACE: return "workspace too small";
+    case KVC_E_HIP: return "HIP launch failure";
+    default: return "unknown status";
+  }
+}
+
+int kvc_plan(const kvc_params_t* params, kvc_layer_t* layers, int num_layers,
+             kvc_plan_info_t* info) {
+  return kvc::plan_impl(params, layers, num_layers, info, true);
+}
+
+int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer_t* layers_dev,
+               int nl, void* ws, size_t ws_bytes, kvc_stream_t stream) {
+  using namespace kvc;
+  kvc_plan_info_t info;
+  int rc = plan_impl(p, const_cast<kvc_layer_t*>(layers), nl, &info, false);
+  if (rc != KVC_OK) return rc;
+  if (nl == 0) return KVC_OK;
+  if (!ws || ws_bytes < info.workspace_bytes) return KVC_E_WORKSPACE;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  char* w = static_cast<char*>(ws);
+  if (!layers_dev) {
+    if (hipMemcpyAsync(w + info.desc_offset, layers, (size_t)nl * sizeof(kvc_layer_t),
+                       hipMemcpyHostToDevice, s) != hipSuccess)
+      return KVC_E_HIP;
+    layers_dev = reinterpret_cast<const kvc_layer_t*>(w + info.desc_offset);
+  }
+  const int es = esize(p->dtype);
+  const int nc = p->head_dim * es / 16;
+  const int H = p->heads;
+  const int BH = p->batch * p->heads;
+  char* norms = w + info.norm_offset;
+  int32_t* idx = reinterpret_cast<int32_t*>(w + info.index_offset);
+  bool any_sel = false;
+  for (int l = 0; l < nl; ++l) any_sel |= layers[l].n_select > 0;
+  (void)hipGetLastError();
+  if ((p->phases & KVC_PHASE_SCORE) && info.score_tiles > 0 && !p->external_index) {
+    if (p->dtype == KVC_BF16)
+      dispatch_nc<KVC_BF16>(nc, true, layers_dev, nl, H, BH, info.score_tiles, norms,
+                            info.norm_row_stride, idx, info.index_row_stride, s);
+    else
+      dispatch_nc<KVC_F32>(nc, true, layers_dev, nl, H, BH, info.score_tiles, norms,
+                           info.norm_row_stride, idx, info.index_row_stride, s);
+  }
+  if ((p->phases & KVC_PHASE_SELECT) && any_sel && !p->external_index) {
+    const dim3 grid((unsigned)info.rows), block(kSelThreads);
+    if (p->dtype == KVC_BF16)
+      hipLaunchKernelGGL(select_kernel<KVC_BF16>, grid, block, 0, s, layers_dev, BH, p->order,
+                         p->algo, norms, info.norm_row_stride, idx, info.index_row_stride);
+    else
+      hipLaunchKernelGGL(select_kernel<KVC_F32>, grid, block, 0, s, layers_dev, BH, p->order,
+                         p->algo, norms, info.norm_row_stride, idx, info.index_row_stride);
+  }
+  if ((p->phases & KVC_PHASE_GATHER) && info.gather_units > 0) {
+    if (p->dtype == KVC_BF16)
+      dispatch_nc<KVC_BF16>(nc, false, layers_dev, nl, H, BH, info.gather_units, norms,
+                            info.norm_row_stride, idx, info.index_row_stride, s);
+    else
+      dispatch_nc<KVC_F32>(nc, false, layers_dev, nl, H, BH, info.gather_units, norms,
+                           info.norm_row_stride, idx, info.index_row_stride, s);
+  }
+  return hipGetLastError() == hipSuccess ? KVC_OK : KVC_E_HIP;
+}
+
+int kvc_compress(const kvc_params_t* params, kvc_layer_t* layers, int num_layers, void* ws,
+                 size_t ws_bytes, kvc_stream_t stream) {
+  kvc_plan_info_t info;
+  const int rc = kvc::plan_impl(params, layers, num_layers, &info, true);
+  if (rc != KVC_OK) return rc;
+  return kvc_launch(params, layers, nullptr, num_layers, ws, ws_bytes, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,166 @@
+"""Batching layer between the reference-shaped compress functions and the HIP engine.
+
+A compress function walks the layers exactly like its reference (same branches, same integer
+arithmetic) and, for every layer that the reference would gather/concatenate, records a
+`Segments` job instead of issuing torch ops.  `execute()` then runs all jobs of the call as ONE
+batched engine launch per (device, dtype, batch, heads, head_dim) group -- score, select and
+gather kernels over every layer at once -- and writes the new (K, V) tensors back into the list.
+"""
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+
+def py_slice(S, start=None, stop=None):
+    """(start, length) of range(S)[start:stop] -- Python/torch slice semantics, incl. `-0:`."""
+    r = range(S)[start:stop]
+    return r.start, len(r)
+
+
+@dataclass
+class Segments:
+    """out = X[:, :, 0:sink_len] ++ X[:, :, zone][selected] ++ X[:, :, tail]  (X = K and V)."""
+    layer_idx: int
+    keys: torch.Tensor
+    values: torch.Tensor
+    sink_len: int = 0
+    zone_start: int = 0
+    zone_len: int = 0
+    n_select: int = 0
+    tail_start: int = 0
+    tail_len: int = 0
+    score_mode: int = N.KVC_SCORE_NORM
+    pool_kernel: int = 0
+    ext_index: Optional[torch.Tensor] = None  # [B, H, n_select] int64 zone-local, ascending
+
+
+_SUPPORTED = {torch.bfloat16: N.KVC_BF16, torch.float32: N.KVC_F32}
+
+
+class PhaseTimer:
+    """When installed with set_phase_timer(), every engine launch is split into its SCORE /
+    SELECT / GATHER kernels with HIP events (torch.cuda.Event, recorded on the stream the
+    kernels run on) around each, so per-kernel durations can be measured live (bench.py)."""
+
+    def __init__(self):
+        self.records = []
+
+    def durations_ms(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, a, b in self.records:
+            out.setdefault(name, []).append(a.elapsed_time(b))
+        return out
+
+
+_timer = None
+
+
+def set_phase_timer(t):
+    global _timer
+    _timer = t
+
+
+def _check_tensors(j: Segments):
+    k, v = j.keys, j.values
+    if not (k.is_cuda and v.is_cuda):
+        raise RuntimeError(
+            f"kvcompress (MI355X HIP engine): layer {j.layer_idx} needs compression but its K/V "
+            f"are on {k.device}/{v.device}; this engine runs on ROCm GPU tensors only "
+            "(no CPU fallback).")
+    if k.dtype not in _SUPPORTED or v.dtype != k.dtype:
+        raise TypeError(
+            f"kvcompress (MI355X HIP engine) supports bfloat16/float32 K and V of one dtype; "
+            f"layer {j.layer_idx} has {k.dtype}/{v.dtype}")
+    if k.dim() != 4 or v.shape != k.shape:
+        raise ValueError(f"layer {j.layer_idx}: K/V must both be [B, H, S, D]; got "
+                         f"{tuple(k.shape)} / {tuple(v.shape)}")
+
+
+def _prep(t):
+    """Last dim contiguous and 16-byte aligned rows (else a device-side contiguous copy)."""
+    es = t.element_size()
+    ok = (t.stride(3) == 1 and t.data_ptr() % 16 == 0 and
+          all((t.stride(d) * es) % 16 == 0 or t.size(d) == 1 for d in range(3)))
+    return t if ok else t.contiguous()
+
+
+def execute(jobs: List[Segments], out_list: list, order: int, algo: int):
+    if not jobs:
+        return
+    groups = {}
+    for j in jobs:
+        _check_tensors(j)
+        B, H, S, D = j.keys.shape
+        groups.setdefault((j.keys.device, j.keys.dtype, B, H, D), []).append(j)
+    for (device, dtype, B, H, D), js in groups.items():
+        _run_group(device, dtype, B, H, D, js, out_list, order, algo)
+
+
+def _run_group(device, dtype, B, H, D, js, out_list, order, algo):
+    n = len(js)
+    external = any(j.ext_index is not None for j in js)
+    if external and not all(j.ext_index is not None or j.n_select == 0 for j in js):
+        raise RuntimeError("mixed external / engine-selected layers in one group")
+    table = np.zeros(n, dtype=N.LAYER_DTYPE)
+    keep = []  # keep prepared inputs alive until the launch is enqueued
+    outs = []
+    for i, j in enumerate(js):
+        k, v = _prep(j.keys), _prep(j.values)
+        keep.append((k, v))
+        n_out = j.sink_len + j.n_select + j.tail_len
+        ko = torch.empty((B, H, n_out, D), dtype=dtype, device=device)
+        vo = torch.empty((B, H, n_out, D), dtype=dtype, device=device)
+        outs.append((ko, vo))
+        t = table[i]
+        t["k"], t["v"] = k.data_ptr(), v.data_ptr()
+        t["k_out"], t["v_out"] = ko.data_ptr(), vo.data_ptr()
+        t["k_stride"] = k.stride()[:3]
+        t["v_stride"] = v.stride()[:3]
+        t["seq_len"] = k.shape[2]
+        t["zone_start"], t["zone_len"], t["n_select"] = j.zone_start, j.zone_len, j.n_select
+        t["sink_len"], t["tail_start"], t["tail_len"] = j.sink_len, j.tail_start, j.tail_len
+        t["pool_kernel"], t["score_mode"] = j.pool_kernel, j.score_mode
+    params = N.Params(dtype=_SUPPORTED[dtype], batch=B, heads=H, head_dim=D, order=order,
+                      algo=algo, phases=N.PHASE_GATHER if external else N.PHASE_ALL,
+                      external_index=1 if external else 0)
+    rc, info = N.plan(params, table)
+    N.check(rc, "kvc_plan")
+    with torch.cuda.device(device):
+        ws = torch.empty(max(int(info.workspace_bytes), 256), dtype=torch.uint8, device=device)
+        tbl = torch.from_numpy(table.view(np.uint8)).pin_memory()
+        ws[info.desc_offset:info.desc_offset + tbl.numel()].copy_(tbl, non_blocking=True)
+        if external:
+            istride = int(info.index_row_stride)
+            iv = ws[info.index_offset:info.index_offset + int(info.rows) * istride * 4]
+            iv = iv.view(torch.int32).view(int(info.rows), istride)
+            for i, j in enumerate(js):
+                if j.n_select:
+                    iv[i * B * H:(i + 1) * B * H, :j.n_select].copy_(
+                        j.ext_index.reshape(B * H, j.n_select))
+        stream = torch.cuda.current_stream(device).cuda_stream
+        dev_tbl = ws.data_ptr() + int(info.desc_offset)
+        if _timer is None:
+            rc = N.launch(params, table, dev_tbl, ws.data_ptr(), int(info.workspace_bytes), stream)
+            N.check(rc, "kvc_launch")
+        else:
+            phases = params.phases
+            for name, bit in (("score", N.PHASE_SCORE), ("select", N.PHASE_SELECT),
+                              ("gather", N.PHASE_GATHER)):
+                if not phases & bit:
+                    continue
+                params.phases = bit
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                rc = N.launch(params, table, dev_tbl, ws.data_ptr(), int(info.workspace_bytes),
+                              stream)
+                b.record()
+                N.check(rc, "kvc_launch")
+                _timer.records.append((name, a, b))
+            params.phases = phases
+    for j, (ko, vo) in zip(js, outs):
+        out_list[j.layer_idx] = (ko, vo)

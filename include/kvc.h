@@ -1,0 +1,150 @@
+/*
+ * kvc.h -- C ABI of the MI355X-native KV-cache compression engine.
+ *
+ * This library is the native half of the drop-in replacement for the reference's
+ * kvcompress/methods hot path (od-liu/CS3602-LLM-Inference-Acceleration).  One call compresses a
+ * batch of layers; each layer's output is built from three segments of its input sequence:
+ *
+ *     out = K[:, :, sink]  ++  K[:, :, zone][selected]  ++  K[:, :, tail]      (same for V)
+ *
+ * which covers every compressing branch of the eight in-scope methods:
+ *   fix_size_l2   fix_size_l2.py:99-152   zone [0,S-P), select keep, tail = last P
+ *   l2_compress   l2_compress.py:227-248  zone [0,S),   select ceil(kr*S)
+ *   h2o_l2        h2o_l2.py:285-325       sink start, zone middle, tail recent
+ *   snapkv_lite   snapkv_lite.py:88-152   zone prefix (snapkv scoring, topk), tail obs window
+ *   pyramid_kv    pyramid_kv.py:300-341   sink, zone middle, tail recent (per-layer size)
+ *   adaptive_l2   adaptive_l2.py:462-546  both branches
+ *   streaming_llm streaming_llm.py:99-109 sink + tail, no selection (pure copy)
+ * recent_only (recent_only.py:65-66) returns views and never reaches the engine.
+ *
+ * The reference does this with torch CPU/GPU ops (torch.norm -> argsort/topk -> sort -> gather
+ * -> cat); the engine reproduces their results bit-exactly, including libstdc++'s introsort /
+ * introselect tie order, torch.norm's 8-lane FMA order, and torch.gather's bf16 NaN rewrite.
+ *
+ * Phases (one HIP kernel each, all stream-ordered on `stream`):
+ *   SCORE  : key L2 norms of every zone token           -> workspace norm region
+ *   SELECT : per (layer,b,h) row: snapkv scoring (opt.), reference-exact k-selection,
+ *            ascending zone-local indices                -> workspace index region (int32)
+ *   GATHER : segment copy of K and V into k_out / v_out (caller-allocated, contiguous)
+ *
+ * Ownership: the caller allocates outputs and the workspace; the library never allocates,
+ * frees or synchronises.  Entry points are reentrant (no global mutable state) and may be used
+ * concurrently on different devices/streams.  All functions return a kvc_status (0 = ok).
+ */
+#ifndef KVC_H
+#define KVC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KVC_ABI_VERSION 1
+
+typedef struct ihipStream_t* kvc_stream_t; /* a hipStream_t; NULL = legacy default stream */
+
+enum kvc_dtype { KVC_F32 = 0, KVC_BF16 = 1 };
+/* KVC_ASC keeps the smallest keys (argsort ascending, "keep_low");
+ * KVC_DESC keeps the largest (argsort descending / topk largest, "keep_high", snapkv). */
+enum kvc_order { KVC_ASC = 0, KVC_DESC = 1 };
+/* KVC_ALGO_SORT: set of argsort(stable=False)[:k] = libstdc++ std::sort (introsort)
+ * KVC_ALGO_TOPK: set of torch.topk = std::nth_element (introselect), or std::partial_sort
+ *                (heap select) when k*64 <= n, exactly as aten TopKImpl.h chooses. */
+enum kvc_algo { KVC_ALGO_SORT = 0, KVC_ALGO_TOPK = 1 };
+enum kvc_score { KVC_SCORE_NORM = 0, KVC_SCORE_SNAPKV = 1 };
+enum kvc_phase {
+  KVC_PHASE_SCORE = 1,
+  KVC_PHASE_SELECT = 2,
+  KVC_PHASE_GATHER = 4,
+  KVC_PHASE_ALL = 7
+};
+enum kvc_status {
+  KVC_OK = 0,
+  KVC_E_ARG = -1,       /* malformed layer table / params                             */
+  KVC_E_DTYPE = -2,     /* dtype is not bf16 / fp32                                   */
+  KVC_E_HEADDIM = -3,   /* head_dim*elem_size not in {128,160,256,320,512} bytes      */
+  KVC_E_ALIGN = -4,     /* a base pointer or stride is not 16-byte aligned            */
+  KVC_E_TOO_LONG = -5,  /* a scored zone is longer than kvc_max_zone_len()            */
+  KVC_E_WORKSPACE = -6, /* workspace smaller than kvc_plan() reported                 */
+  KVC_E_HIP = -7        /* a HIP launch failed                                        */
+};
+
+/* One layer.  Inputs K,V: [batch, heads, seq_len, head_dim], last dim contiguous, arbitrary
+ * element strides for the other three dims.  Outputs: contiguous [batch, heads, n_out, head_dim]
+ * with n_out = sink_len + n_select + tail_len. */
+typedef struct kvc_layer {
+  const void* k;
+  const void* v;
+  void* k_out;
+  void* v_out;
+  int64_t k_stride[3]; /* element strides of dims batch, heads, seq */
+  int64_t v_stride[3];
+  int32_t seq_len;     /* S */
+  int32_t zone_start;  /* scored zone [zone_start, zone_start + zone_len) */
+  int32_t zone_len;
+  int32_t n_select;    /* tokens kept from the zone: 0 <= n_select <= zone_len */
+  int32_t sink_len;    /* segment A: source rows [0, sink_len)                   */
+  int32_t tail_start;  /* segment C: source rows [tail_start, tail_start+tail_len) */
+  int32_t tail_len;
+  int32_t pool_kernel; /* KVC_SCORE_SNAPKV: avg_pool1d kernel; <= 1 means no pooling */
+  int32_t score_mode;  /* enum kvc_score */
+  /* ---- filled in by kvc_plan() ---- */
+  int32_t n_out;
+  int32_t row0;  /* first workspace row of this layer (rows = layer*batch*heads + b*heads + h) */
+  int32_t tile0; /* first 64-token SCORE tile of this layer */
+  int64_t unit0; /* first GATHER unit (one 16-byte chunk of one output row of K or V) */
+} kvc_layer_t;
+
+typedef struct kvc_params {
+  int32_t dtype;
+  int32_t batch;
+  int32_t heads;
+  int32_t head_dim;
+  int32_t order;          /* enum kvc_order */
+  int32_t algo;           /* enum kvc_algo  */
+  int32_t phases;         /* OR of enum kvc_phase */
+  int32_t external_index; /* 1: GATHER reads indices the caller wrote into the index region */
+} kvc_params_t;
+
+typedef struct kvc_plan_info {
+  size_t desc_offset;      /* workspace byte offset of the device copy of the layer table */
+  size_t norm_offset;      /* workspace byte offset of the norm region                    */
+  size_t index_offset;     /* workspace byte offset of the int32 index region             */
+  size_t workspace_bytes;  /* total workspace the launch needs                              */
+  int64_t norm_row_stride; /* elements (of dtype) per row in the norm region               */
+  int64_t index_row_stride;/* int32 entries per row in the index region                   */
+  int64_t rows;            /* num_layers * batch * heads                                   */
+  int64_t score_tiles;     /* SCORE work items                                             */
+  int64_t gather_units;    /* GATHER work items                                            */
+} kvc_plan_info_t;
+
+/* ABI/library identification. */
+int kvc_version(void);
+size_t kvc_layer_struct_size(void);
+int kvc_max_zone_len(void);
+const char* kvc_status_string(int status);
+
+/* Validates the table, fills the kvc_plan() fields of every layer (host memory) and the
+ * workspace layout.  Pure host function. */
+int kvc_plan(const kvc_params_t* params, kvc_layer_t* layers, int num_layers,
+             kvc_plan_info_t* info);
+
+/* Launches the requested phases.  `layers` is the host table filled by kvc_plan();
+ * `layers_dev` is a device copy of it (e.g. at workspace + info.desc_offset) that the caller
+ * has already made stream-ordered with this launch.  Passing layers_dev = NULL makes the library
+ * enqueue that copy itself (hipMemcpyAsync from `layers` into the workspace). */
+int kvc_launch(const kvc_params_t* params, const kvc_layer_t* layers,
+               const kvc_layer_t* layers_dev, int num_layers, void* workspace,
+               size_t workspace_bytes, kvc_stream_t stream);
+
+/* Convenience: kvc_plan + kvc_launch(layers_dev = NULL).  `layers` is updated in place. */
+int kvc_compress(const kvc_params_t* params, kvc_layer_t* layers, int num_layers,
+                 void* workspace, size_t workspace_bytes, kvc_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KVC_H */

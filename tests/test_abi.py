@@ -1,0 +1,104 @@
+"""CPU-side checks of the C ABI: the library loads, exports every symbol include/kvc.h declares,
+its struct layout matches, and kvc_plan (a pure host function) validates and plans correctly."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from kvcompress import _native as N
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_functions():
+    src = open(os.path.join(ROOT, "include", "kvc.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(kvc_[a-z_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = N.lib()
+    declared = _declared_functions()
+    assert set(declared) == set(N.EXPORTS)
+    for name in declared:
+        assert hasattr(L, name), name
+
+
+def test_struct_layout():
+    L = N.lib()
+    assert L.kvc_layer_struct_size() == N.LAYER_DTYPE.itemsize == 136
+    assert ctypes.sizeof(N.Params) == 32
+    assert ctypes.sizeof(N.PlanInfo) == 72
+    assert L.kvc_version() == 1
+    assert L.kvc_max_zone_len() == 16384
+
+
+def _layer(S, zs, zl, k, sink=0, ts=0, tl=0, ptr=4096):
+    t = np.zeros(1, dtype=N.LAYER_DTYPE)[0]
+    t["k"] = t["v"] = t["k_out"] = t["v_out"] = ptr
+    t["k_stride"] = t["v_stride"] = (32 * S * 128, S * 128, 128)
+    t["seq_len"], t["zone_start"], t["zone_len"], t["n_select"] = S, zs, zl, k
+    t["sink_len"], t["tail_start"], t["tail_len"] = sink, ts, tl
+    return t
+
+
+def _params(**kw):
+    d = dict(dtype=N.KVC_BF16, batch=1, heads=32, head_dim=128, order=0, algo=0,
+             phases=N.PHASE_ALL, external_index=0)
+    d.update(kw)
+    return N.Params(**d)
+
+
+def test_plan_fills_prefix_fields_and_layout():
+    table = np.array([_layer(16384, 0, 16384, 512), _layer(4096, 4, 3648, 64, 4, 3652, 444),
+                      _layer(2048, 0, 0, 0, 4, 1028, 1020)], dtype=N.LAYER_DTYPE)
+    rc, info = N.plan(_params(), table)
+    assert rc == 0
+    assert list(table["n_out"]) == [512, 512, 1024]
+    assert list(table["row0"]) == [0, 32, 64]
+    assert list(table["tile0"]) == [0, 32 * 256, 32 * 256 + 32 * 57]
+    assert info.score_tiles == 32 * 256 + 32 * 57
+    assert list(table["unit0"]) == [0, 2 * 32 * 512 * 16, 4 * 32 * 512 * 16]
+    assert info.gather_units == 2 * 32 * 16 * (512 + 512 + 1024)
+    assert info.rows == 96 and info.norm_row_stride == 16384 and info.index_row_stride == 512
+    assert info.norm_offset >= 3 * 136 and info.index_offset >= info.norm_offset + 96 * 16384 * 2
+
+
+@pytest.mark.parametrize("bad, code", [
+    (dict(dtype=5), -2), (dict(head_dim=96), -3), (dict(head_dim=100), -3), (dict(batch=0), -1),
+    (dict(order=3), -1), (dict(algo=9), -1)])
+def test_plan_rejects_bad_params(bad, code):
+    table = np.array([_layer(100, 0, 100, 10)], dtype=N.LAYER_DTYPE)
+    rc, _ = N.plan(_params(**bad), table)
+    assert rc == code
+
+
+def test_plan_rejects_bad_layers():
+    cases = [
+        (_layer(100, 0, 101, 10), -1),                 # zone past the end
+        (_layer(100, 0, 100, 101), -1),                # selecting more than the zone
+        (_layer(100, 0, 100, 10, ts=95, tl=10), -1),   # tail past the end
+        (_layer(100, 0, 100, 10, ptr=4100), -4),       # misaligned pointer
+        (_layer(20000, 0, 20000, 10), -5),             # zone longer than LDS-resident limit
+    ]
+    for t, code in cases:
+        rc, _ = N.plan(_params(), np.array([t], dtype=N.LAYER_DTYPE))
+        assert rc == code, (t, rc)
+    # select-all and pure-copy layers may be longer than the LDS limit (no selection runs)
+    rc, _ = N.plan(_params(), np.array([_layer(20000, 0, 20000, 20000)], dtype=N.LAYER_DTYPE))
+    assert rc == 0
+
+
+def test_status_strings():
+    for code in range(-7, 1):
+        assert N.status_string(code)
+
+
+def test_launch_revalidates_against_plan():
+    table = np.array([_layer(100, 0, 100, 10)], dtype=N.LAYER_DTYPE)
+    rc, info = N.plan(_params(), table)
+    assert rc == 0
+    table["unit0"] = 7  # tampered plan fields are rejected before any HIP call
+    assert N.launch(_params(), table, 0, 0, 0, 0) == -1

@@ -1,0 +1,22 @@
+#!/bin/bash
+# One GPU-box pass: parity tests, headline bench, rocprofv3 kernel stats.  Every GPU step has
+# its own time limit and the steps are chained so the first failure ends the call.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+R="${GRAFT_REPO_ROOT:-/root/repo}"
+MODE="${1:-all}"
+if [ "$MODE" = "all" ] || [ "$MODE" = "test" ]; then
+  timeout -k 10 900 python -m pytest tests -m gpu -q -rf --timeout=300 -p no:cacheprovider \
+      > gpurun_out/pytest_gpu.log 2>&1
+  rc=$?; tail -5 gpurun_out/pytest_gpu.log; [ $rc -ne 0 ] && [ "$MODE" = "test" ] && exit $rc
+  [ $rc -gt 1 ] && exit $rc
+fi
+if [ "$MODE" = "all" ] || [ "$MODE" = "bench" ]; then
+  timeout -k 10 400 python bench.py --steps 10 --warmup 3 > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
+  cat gpurun_out/bench.json
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run \
+      -- python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$R/gpurun_out/prof.log" 2>&1 || exit $?
+  find "$R/gpurun_out/prof" -name "*stats*" | head
+fi
