@@ -37,7 +37,9 @@ def algorithmic_bytes(es=2):
 def cpu_baseline(seconds=12.0):
     """The reference's CPU op sequence (oracle/torch_port.py) on this host's cores, bounded."""
     from oracle.torch_port import fix_size_l2_layer
-    threads = len(os.sched_getaffinity(0))
+    # the GPU box exposes the whole machine's CPUs but grants one GPU a 16-core share
+    # (OMP_NUM_THREADS is set to it there)
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(0)
     k = torch.randn(B, H, S, D, generator=g).to(torch.bfloat16)

@@ -17,6 +17,7 @@
 //                   torch.cat of the reference, e.g. fix_size_l2.py:137-147).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "kvc.h"
@@ -31,7 +32,9 @@ constexpr int kScoreWaves = kScoreThreads / 64;
 constexpr int kSelThreads = 1024;
 constexpr int kSelWaves = kSelThreads / 64;
 constexpr int kZoneMax = 16384;  // longest zone whose keys fit the select kernel's LDS
+constexpr int kWaveSeg = 1024;   // segments this short are finished by one wave (no block barriers)
 constexpr int kGatherThreads = 256;
+constexpr int kGatherTokens = 64;  // output tokens per gather block
 constexpr int kBig = 0x7FFFFFFF;
 
 template <int DT>
@@ -184,7 +187,7 @@ __global__ void __launch_bounds__(kScoreThreads)
 // ---------------------------------------------------------------------------------------------
 template <typename KeyT>
 struct SelScalars {
-  int lo, hi, state, m, gnext;
+  int lo, hi, state, m, gnext, depth;
   KeyT p;
   int wa[kSelWaves];
   int wb[kSelWaves];
@@ -258,6 +261,104 @@ __device__ void snapkv_keys(const char* nrow, int n, int pool_k, bool desc, KeyT
   }
 }
 
+// The rest of the partition chain once the straddling segment is <= kWaveSeg long, run by one
+// wave (64 lanes x <= 16 positions) with wave-level synchronisation only.  Same algorithm as the
+// block-level loop in select_kernel; lo/hi/depth are uniform across the wave's lanes.
+template <typename KeyT>
+__device__ void wave_chain(KeyT* key, uint16_t* idx, uint16_t* spos, int k, bool topk, int thr,
+                           int lo, int hi, int depth, SelScalars<KeyT>& sc) {
+  const int lane = threadIdx.x & 63;
+  int msw = 0, gnext = kBig;
+  bool first = true;
+  while (true) {
+    if (!first) {
+      const int cut = min(gnext, msw > 0 ? (int)spos[msw] : kBig);
+      if (topk) {
+        if (cut <= k - 1) lo = cut; else hi = cut;
+      } else {
+        if (k <= cut) hi = cut; else lo = cut;
+      }
+    }
+    first = false;
+    if (lo == k || hi == k) break;
+    if (hi - lo <= thr) {
+      if (lane == 0) insertion_sort(key, idx, lo, hi);
+      break;
+    }
+    if (depth == 0) {
+      if (lane == 0) {
+        if (topk) {
+          heap_select(key + lo, idx + lo, k - lo, hi - lo);
+          kv_swap(key, idx, lo, k - 1);
+        } else {
+          make_heap(key + lo, idx + lo, hi - lo);
+          sort_heap(key + lo, idx + lo, hi - lo);
+        }
+      }
+      break;
+    }
+    --depth;
+    if (lane == 0) {
+      move_median_to_first(key, idx, lo, lo + 1, lo + (hi - lo) / 2, hi - 1);
+      sc.gnext = kBig;
+    }
+    wave_sync();
+    const KeyT p = key[lo];
+    const int J = (hi - lo - 1 + 63) / 64;  // <= 16
+    uint32_t gem = 0, lem = 0;
+    int tot_le = 0;
+    for (int j = 0; j < J; ++j) {
+      const int pos = lo + 1 + j * 64 + lane;
+      const bool valid = pos < hi;
+      const KeyT kk = valid ? key[pos] : (KeyT)0;
+      const bool ge = valid && !(kk < p);
+      const bool le = valid && !(p < kk);
+      gem |= (uint32_t)ge << j;
+      lem |= (uint32_t)le << j;
+      tot_le += __popcll(__ballot(le));
+    }
+    int run = 0;
+    for (int j = 0; j < J; ++j) {
+      const bool le = (lem >> j) & 1u;
+      const uint64_t bl = __ballot(le);
+      if (le) {
+        const int incl = run + __popcll(bl & lanemask_le(lane));
+        spos[tot_le - incl + 1] = (uint16_t)(lo + 1 + j * 64 + lane);
+      }
+      run += __popcll(bl);
+    }
+    if (lane == 0) spos[tot_le + 1] = (uint16_t)lo;
+    wave_sync();
+    run = 0;
+    msw = 0;
+    for (int j = 0; j < J; ++j) {
+      const bool ge = (gem >> j) & 1u;
+      const uint64_t bg = __ballot(ge);
+      const int t = run + __popcll(bg & lanemask_lt(lane)) + 1;
+      const bool pair = ge && t <= tot_le + 1 && (int)spos[t] > lo + 1 + j * 64 + lane;
+      msw += __popcll(__ballot(pair));
+      run += __popcll(bg);
+    }
+    run = 0;
+    for (int j = 0; j < J; ++j) {
+      const bool ge = (gem >> j) & 1u;
+      const uint64_t bg = __ballot(ge);
+      if (ge) {
+        const int t = run + __popcll(bg & lanemask_lt(lane)) + 1;
+        const int pos = lo + 1 + j * 64 + lane;
+        if (t <= msw)
+          kv_swap(key, idx, pos, (int)spos[t]);
+        else if (t == msw + 1)
+          sc.gnext = pos;
+      }
+      run += __popcll(bg);
+    }
+    wave_sync();
+    gnext = sc.gnext;
+  }
+  wave_sync();
+}
+
 template <int DT>
 __global__ void __launch_bounds__(kSelThreads)
     select_kernel(const kvc_layer_t* __restrict__ L, int BH, int order, int algo,
@@ -329,8 +430,11 @@ __global__ void __launch_bounds__(kSelThreads)
         }
         if (lo == k || hi == k) {
           // a partition boundary sits exactly at k: the first-k set is final
-        } else if (hi - lo <= thr) {
-          insertion_sort(key, idx, lo, hi);  // final insertion sort (stable) of the segment
+        } else if (hi - lo <= kWaveSeg) {
+          state = 2;  // short segment: wave 0 finishes the chain without block barriers
+          sc.lo = lo;
+          sc.hi = hi;
+          sc.depth = depth;
         } else if (depth == 0) {  // depth limit: libstdc++ switches to heap algorithms
           if (topk) {
             heap_select(key + lo, idx + lo, k - lo, hi - lo);
@@ -441,6 +545,8 @@ __global__ void __launch_bounds__(kSelThreads)
     }
     __syncthreads();
   }
+  if (sc.state == 2 && wid == 0) wave_chain(key, idx, spos, k, topk, thr, sc.lo, sc.hi, sc.depth, sc);
+  __syncthreads();
 
   // ---- emit the kept set {idx[0..k)} as ascending zone-local indices ----
   uint16_t* flag = spos;
@@ -475,59 +581,116 @@ __global__ void __launch_bounds__(kSelThreads)
 // ---------------------------------------------------------------------------------------------
 template <int DT, int NC>
 __global__ void __launch_bounds__(kGatherThreads)
-    gather_kernel(const kvc_layer_t* __restrict__ L, int nl, int H, int BH,
-                  const int32_t* __restrict__ gidx, int64_t idx_stride, int64_t total) {
+    gather_kernel(const kvc_layer_t* __restrict__ L, int H, int BH,
+                  const int32_t* __restrict__ gidx, int64_t idx_stride) {
+  // grid = (rows, output-token blocks); one block copies kGatherTokens output rows of K and V
   constexpr int ESZ = DTypeTraits<DT>::esz;
-  for (int64_t u = (int64_t)blockIdx.x * kGatherThreads + threadIdx.x; u < total;
-       u += (int64_t)gridDim.x * kGatherThreads) {
-    int lo = 0, hi = nl - 1;  // largest layer with unit0 <= u
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (L[mid].unit0 <= u)
-        lo = mid;
-      else
-        hi = mid - 1;
-    }
-    const kvc_layer_t* ly = L + lo;
-    const int n_out = ly->n_out;
-    const int per_row = n_out * NC;
-    int r = (int)(u - ly->unit0);
-    const int is_v = r >= BH * per_row;
-    if (is_v) r -= BH * per_row;
-    const int row = r / per_row;
-    r -= row * per_row;
-    const int t = r / NC;
-    const int c = r - t * NC;
-    const int b = row / H, h = row - (row / H) * H;
-    int src;
-    bool gathered = false;
-    if (t < ly->sink_len) {
-      src = t;
-    } else if (t < ly->sink_len + ly->n_select) {
-      int zi = gidx[(int64_t)(ly->row0 + row) * idx_stride + (t - ly->sink_len)];
-      zi = min(max(zi, 0), ly->zone_len - 1);  // never read outside the zone, whatever the index
-      src = ly->zone_start + zi;
-      gathered = true;
-    } else {
-      src = ly->tail_start + (t - ly->sink_len - ly->n_select);
-    }
-    const int64_t* st = is_v ? ly->v_stride : ly->k_stride;
-    const char* sp = static_cast<const char*>(is_v ? ly->v : ly->k) +
-                     ((int64_t)b * st[0] + (int64_t)h * st[1] + (int64_t)src * st[2]) * ESZ +
-                     c * 16;
-    uint4 x = *reinterpret_cast<const uint4*>(sp);
-    if constexpr (DT == KVC_BF16) {
-      if (gathered) {
-        x.x = canon_nan_bf16x2(x.x);
-        x.y = canon_nan_bf16x2(x.y);
-        x.z = canon_nan_bf16x2(x.z);
-        x.w = canon_nan_bf16x2(x.w);
+  constexpr int ITERS = (kGatherTokens * NC + kGatherThreads - 1) / kGatherThreads;
+  const int grow = blockIdx.x;
+  const kvc_layer_t* ly = L + grow / BH;
+  const int r = grow - (grow / BH) * BH;
+  const int n_out = ly->n_out;
+  const int t0 = blockIdx.y * kGatherTokens;
+  if (t0 >= n_out) return;
+  const int nu = min(kGatherTokens, n_out - t0) * NC;
+  const int b = r / H, h = r - (r / H) * H;
+  const int sink = ly->sink_len, nsel = ly->n_select;
+  const char* kb = static_cast<const char*>(ly->k) +
+                   ((int64_t)b * ly->k_stride[0] + (int64_t)h * ly->k_stride[1]) * ESZ;
+  const char* vb = static_cast<const char*>(ly->v) +
+                   ((int64_t)b * ly->v_stride[0] + (int64_t)h * ly->v_stride[1]) * ESZ;
+  const int64_t kss = ly->k_stride[2] * ESZ, vss = ly->v_stride[2] * ESZ;
+  const int32_t* irow = gidx + (int64_t)(ly->row0 + r) * idx_stride;
+  const int64_t obase = ((int64_t)r * n_out + t0) * NC * 16;
+  char* ko = static_cast<char*>(ly->k_out) + obase;
+  char* vo = static_cast<char*>(ly->v_out) + obase;
+  uint4 xk[ITERS], xv[ITERS];
+  bool gat[ITERS];
+#pragma unroll
+  for (int i = 0; i < ITERS; ++i) {
+    const int u = threadIdx.x + i * kGatherThreads;
+    gat[i] = false;
+    if (u < nu) {
+      const int t = t0 + u / NC, c = u - (u / NC) * NC;
+      int src;
+      if (t < sink) {
+        src = t;
+      } else if (t < sink + nsel) {
+        int zi = irow[t - sink];
+        zi = min(max(zi, 0), ly->zone_len - 1);  // never read outside the zone
+        src = ly->zone_start + zi;
+        gat[i] = true;
+      } else {
+        src = ly->tail_start + (t - sink - nsel);
       }
+      xk[i] = *reinterpret_cast<const uint4*>(kb + src * kss + c * 16);
+      xv[i] = *reinterpret_cast<const uint4*>(vb + src * vss + c * 16);
     }
-    char* dp = static_cast<char*>(is_v ? ly->v_out : ly->k_out) +
-               (((int64_t)row * n_out + t) * NC + c) * 16;
-    *reinterpret_cast<uint4*>(dp) = x;
   }
+#pragma unroll
+  for (int i = 0; i < ITERS; ++i) {
+    const int u = threadIdx.x + i * kGatherThreads;
+    if (u < nu) {
+      uint4 a = xk[i], bq = xv[i];
+      if constexpr (DT == KVC_BF16) {
+        if (gat[i]) {  // torch.gather's bf16 NaN rewrite (gathered segment only)
+          a.x = canon_nan_bf16x2(a.x); a.y = canon_nan_bf16x2(a.y);
+          a.z = canon_nan_bf16x2(a.z); a.w = canon_nan_bf16x2(a.w);
+          bq.x = canon_nan_bf16x2(bq.x); bq.y = canon_nan_bf16x2(bq.y);
+          bq.z = canon_nan_bf16x2(bq.z); bq.w = canon_nan_bf16x2(bq.w);
+        }
+      }
+      *reinterpret_cast<uint4*>(ko + (int64_t)u * 16) = a;
+      *reinterpret_cast<uint4*>(vo + (int64_t)u * 16) = bq;
+    }
+  }
+}
+
+// Experimental SCORE variant (KVC_SCORE_VARIANT=direct): each lane streams its own token row
+// with 16-B loads straight to registers (no LDS transpose); one wave instruction then touches
+// 64 rows.  Kept to measure whether a fused per-row design can skip the LDS slab.
+template <int DT, int NC>
+__global__ void __launch_bounds__(kScoreThreads)
+    score_direct_kernel(const kvc_layer_t* __restrict__ L, int nl, int H, int64_t total_tiles,
+                        char* __restrict__ norms, int64_t norm_stride) {
+  constexpr int ESZ = DTypeTraits<DT>::esz;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t g = (int64_t)blockIdx.x * kScoreWaves + wid;
+  if (g >= total_tiles) return;
+  int lo = 0, hi = nl - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (L[mid].tile0 <= g) lo = mid; else hi = mid - 1;
+  }
+  const kvc_layer_t* ly = L + lo;
+  const int zlen = ly->zone_len;
+  const int tpr = (zlen + kTile - 1) / kTile;
+  const int local = (int)(g - ly->tile0);
+  const int row = local / tpr;
+  const int tt = local - row * tpr;
+  const int b = row / H, h = row - (row / H) * H;
+  const int tok0 = tt * kTile;
+  const int ntok = min(kTile, zlen - tok0);
+  if (lane >= ntok) return;
+  const char* p = static_cast<const char*>(ly->k) +
+                  ((int64_t)b * ly->k_stride[0] + (int64_t)h * ly->k_stride[1] +
+                   (int64_t)(ly->zone_start + tok0 + lane) * ly->k_stride[2]) * ESZ;
+  uint4 x[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) x[c] = *reinterpret_cast<const uint4*>(p + c * 16);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < NC; ++c) accum_chunk<DT, NC>(acc, x[c], c);
+  float s = acc[0];
+#pragma unroll
+  for (int j = 1; j < 8; ++j) s = s + acc[j];
+  const float r = __builtin_sqrtf(s);
+  char* nrow = norms + (int64_t)(ly->row0 + row) * norm_stride * ESZ;
+  if constexpr (DT == KVC_BF16)
+    reinterpret_cast<uint16_t*>(nrow)[tok0 + lane] = (uint16_t)f32_to_bf16_rne(r);
+  else
+    reinterpret_cast<float*>(nrow)[tok0 + lane] = r;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -614,17 +777,22 @@ template <int DT, int NC>
 static void launch_score(const kvc_layer_t* Ld, int nl, int H, int64_t tiles, char* norms,
                          int64_t nstride, hipStream_t s) {
   const unsigned grid = (unsigned)((tiles + kScoreWaves - 1) / kScoreWaves);
-  hipLaunchKernelGGL((score_kernel<DT, NC>), dim3(grid), dim3(kScoreThreads), 0, s, Ld, nl, H,
-                     tiles, norms, nstride);
+  const char* var = getenv("KVC_SCORE_VARIANT");
+  if (var && strcmp(var, "direct") == 0)
+    hipLaunchKernelGGL((score_direct_kernel<DT, NC>), dim3(grid), dim3(kScoreThreads), 0, s, Ld,
+                       nl, H, tiles, norms, nstride);
+  else
+    hipLaunchKernelGGL((score_kernel<DT, NC>), dim3(grid), dim3(kScoreThreads), 0, s, Ld, nl, H,
+                       tiles, norms, nstride);
 }
 
+// `work` = max n_out over layers; grid = (rows, token blocks)
 template <int DT, int NC>
 static void launch_gather(const kvc_layer_t* Ld, int nl, int H, int BH, const int32_t* idx,
-                          int64_t istride, int64_t units, hipStream_t s) {
-  int64_t blocks = (units + kGatherThreads - 1) / kGatherThreads;
-  if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL((gather_kernel<DT, NC>), dim3((unsigned)blocks), dim3(kGatherThreads), 0, s,
-                     Ld, nl, H, BH, idx, istride, units);
+                          int64_t istride, int64_t work, hipStream_t s) {
+  const dim3 grid((unsigned)(nl * BH), (unsigned)((work + kGatherTokens - 1) / kGatherTokens));
+  hipLaunchKernelGGL((gather_kernel<DT, NC>), grid, dim3(kGatherThreads), 0, s, Ld, H, BH, idx,
+                     istride);
 }
 
 template <int DT>
@@ -720,11 +888,13 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
                          p->algo, norms, info.norm_row_stride, idx, info.index_row_stride);
   }
   if ((p->phases & KVC_PHASE_GATHER) && info.gather_units > 0) {
+    int64_t max_out = 0;
+    for (int l = 0; l < nl; ++l) max_out = layers[l].n_out > max_out ? layers[l].n_out : max_out;
     if (p->dtype == KVC_BF16)
-      dispatch_nc<KVC_BF16>(nc, false, layers_dev, nl, H, BH, info.gather_units, norms,
+      dispatch_nc<KVC_BF16>(nc, false, layers_dev, nl, H, BH, max_out, norms,
                             info.norm_row_stride, idx, info.index_row_stride, s);
     else
-      dispatch_nc<KVC_F32>(nc, false, layers_dev, nl, H, BH, info.gather_units, norms,
+      dispatch_nc<KVC_F32>(nc, false, layers_dev, nl, H, BH, max_out, norms,
                            info.norm_row_stride, idx, info.index_row_stride, s);
   }
   return hipGetLastError() == hipSuccess ? KVC_OK : KVC_E_HIP;

@@ -182,3 +182,40 @@ int orc_snapkv_scores(int dtype, const void* norms, int64_t n, int64_t pool_k, v
 }
 
 }  // extern "C"
+
+// ---- adversarial inputs (test infrastructure) ----
+// McIlroy's "killer adversary for quicksort" (Software: Practice & Experience 29(4), 1999) run
+// against libstdc++ std::sort (asc) / std::nth_element: lazily freezes values during the sort so
+// median-of-3 pivots are poor, driving introsort into its depth-limit heapsort fallback.
+// Writes a permutation of 0..n-1 to out.
+namespace {
+struct Adversary {
+  std::vector<int64_t> val;
+  int64_t gas, nsolid = 0, candidate = 0;
+  explicit Adversary(int64_t n) : val(n, n), gas(n) {}
+  bool less(int64_t x, int64_t y) {
+    if (val[x] == gas && val[y] == gas) {
+      if (x == candidate) val[x] = nsolid++;
+      else val[y] = nsolid++;
+    }
+    if (val[x] == gas) candidate = x;
+    else if (val[y] == gas) candidate = y;
+    return val[x] < val[y];
+  }
+};
+}  // namespace
+
+extern "C" int orc_antiqsort(int64_t n, int mode, int64_t k, int64_t* out) {
+  Adversary a(n);
+  std::vector<int64_t> ix(n);
+  for (int64_t i = 0; i < n; ++i) ix[i] = i;
+  auto cmp = [&a](int64_t x, int64_t y) { return a.less(x, y); };
+  if (mode == 0)
+    std::sort(ix.begin(), ix.end(), cmp);
+  else
+    std::nth_element(ix.begin(), ix.begin() + (k > 0 ? k - 1 : 0), ix.end(), cmp);
+  for (int64_t i = 0; i < n; ++i)
+    if (a.val[i] == a.gas) a.val[i] = a.nsolid++;
+  for (int64_t i = 0; i < n; ++i) out[i] = a.val[i];
+  return 0;
+}

@@ -41,6 +41,7 @@ def lib():
         _LIB.orc_sort_prefix.argtypes = [ctypes.c_int, vp, i64, i64, ctypes.c_int, vp]
         _LIB.orc_topk.argtypes = [ctypes.c_int, vp, i64, i64, ctypes.c_int, vp]
         _LIB.orc_snapkv_scores.argtypes = [ctypes.c_int, vp, i64, i64, vp]
+        _LIB.orc_antiqsort.argtypes = [i64, ctypes.c_int, i64, vp]
     return _LIB
 
 

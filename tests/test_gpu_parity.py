@@ -184,3 +184,23 @@ def test_no_cpu_fallback():
     K = torch.zeros(1, 2, 100, 64, dtype=torch.bfloat16)
     with pytest.raises(RuntimeError, match="ROCm GPU tensors only"):
         fix_size_l2_compress([(K, K)], fix_kv_size=10, skip_layers=[])
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_abi_adversarial_depth_limit(mode):
+    """McIlroy-adversary keys drive libstdc++ into its depth-limit heap fallback; the device
+    emulation (serial heap code in the select kernel) must land on the same set."""
+    n = 4096
+    adv = np.empty(n, dtype=np.int64)
+    for k in (1, 100, n // 3, n // 2, n - 1):
+        oracle.lib().orc_antiqsort(n, mode, k, adv.ctypes.data)
+        K = np.zeros((1, 1, n, 64), dtype=np.float32)
+        K[0, 0, :, 0] = (adv + 1).astype(np.float32)  # norm == adv + 1 exactly (< 2^12)
+        # ascending sort keeps the smallest; topk keeps the largest -> feed -key order via desc
+        nrm, idx = _abi_select(K, k, 0, mode)
+        np.testing.assert_array_equal(nrm[0, 0], (adv + 1).astype(np.float32))
+        if mode == 0:
+            ref = np.sort(oracle.argsort_prefix(nrm, k), axis=-1)
+        else:  # ascending topk == torch.topk(-x): use the oracle's topk on negated values
+            ref = np.sort(oracle.topk_indices(-nrm, k), axis=-1)
+        np.testing.assert_array_equal(idx, ref, err_msg=f"mode={mode} k={k}")

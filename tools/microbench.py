@@ -1,0 +1,38 @@
+"""Interleaved A/B timing of engine kernel variants on the headline workload (one process,
+rounds interleaved; cdna_hip_programming.md §5.4 rule 24).  GPU box only."""
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cs3602-llm-inference-acceleration_amd"))
+from kvcompress import _engine  # noqa: E402
+from kvcompress.methods import fix_size_l2_compress  # noqa: E402
+
+variants = sys.argv[1].split(",") if len(sys.argv) > 1 else ["lds", "direct"]
+rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+dev = torch.device("cuda:0")
+g = torch.Generator(device=dev).manual_seed(0)
+layers = [(torch.randn(1, 32, 16384, 128, device=dev, generator=g).to(torch.bfloat16),
+           torch.randn(1, 32, 16384, 128, device=dev, generator=g).to(torch.bfloat16))
+          for _ in range(32)]
+res = {v: {} for v in variants}
+ref = None
+for r in range(rounds):
+    for v in variants:
+        os.environ["KVC_SCORE_VARIANT"] = v
+        t = _engine.PhaseTimer()
+        _engine.set_phase_timer(t)
+        for _ in range(5):
+            out = fix_size_l2_compress(layers, fix_kv_size=512, skip_layers=[])
+        _engine.set_phase_timer(None)
+        d = t.durations_ms()
+        for ph, xs in d.items():
+            res[v].setdefault(ph, []).append(min(xs))
+        if ref is None:
+            ref = [(a.clone(), b.clone()) for a, b in out]
+        else:
+            assert all(torch.equal(a, c) and torch.equal(b, e) for (a, b), (c, e) in zip(out, ref))
+print(json.dumps({v: {ph: sorted(x)[len(x) // 2] for ph, x in d.items()} for v, d in res.items()}))
