@@ -74,6 +74,19 @@ __device__ __forceinline__ typename DTypeTraits<DT>::key_t key_of(float f, bool 
     return key_f32(f32_to_bits(f), desc);
 }
 
+// Diagnostic build only (-DKVC_STAMPS): thread 0 of every select workgroup records s_memtime at
+// phase boundaries into a per-row slot after the index region; the product build has no stamps.
+#ifdef KVC_STAMPS
+#define KVC_STAMP(i)                                                             \
+  do {                                                                           \
+    if (stamps && threadIdx.x == 0) stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define KVC_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -363,7 +376,7 @@ template <int DT>
 __global__ void __launch_bounds__(kSelThreads)
     select_kernel(const kvc_layer_t* __restrict__ L, int BH, int order, int algo,
                   const char* __restrict__ norms, int64_t norm_stride,
-                  int32_t* __restrict__ out_idx, int64_t idx_stride) {
+                  int32_t* __restrict__ out_idx, int64_t idx_stride, uint64_t* stamps) {
   typedef typename DTypeTraits<DT>::key_t KeyT;
   constexpr int ESZ = DTypeTraits<DT>::esz;
   // LDS: key[kZoneMax] | idx[kZoneMax] (u16) | spos[kZoneMax + 8] (u16) | scalars
@@ -377,6 +390,7 @@ __global__ void __launch_bounds__(kSelThreads)
   uint16_t* spos = reinterpret_cast<uint16_t*>(smem + KEY_B + IDX_B);
 
   const int row = blockIdx.x;
+  KVC_STAMP(0);
   const kvc_layer_t* ly = L + row / BH;
   const int n = ly->zone_len;
   const int k = ly->n_select;
@@ -398,15 +412,45 @@ __global__ void __launch_bounds__(kSelThreads)
     __syncthreads();
     for (int i = tid; i < n; i += kSelThreads) idx[i] = (uint16_t)i;
   } else {
-    for (int i = tid; i < n; i += kSelThreads) {
-      if constexpr (DT == KVC_BF16)
-        key[i] = key_bf16(reinterpret_cast<const uint16_t*>(nrow)[i], desc);
-      else
-        key[i] = key_f32(reinterpret_cast<const uint32_t*>(nrow)[i], desc);
-      idx[i] = (uint16_t)i;
+    // 16-B loads, all issued before the first use (norm rows are padded to 64 elements, so a
+    // whole vector past n stays inside the row); keys/indices written as 16-B LDS stores
+    constexpr int VEC = 16 / ESZ;
+    constexpr int MAXV = (kZoneMax / VEC + kSelThreads - 1) / kSelThreads;
+    const int nvec = (n + VEC - 1) / VEC;
+    uint4 buf[MAXV];
+#pragma unroll
+    for (int q = 0; q < MAXV; ++q) {
+      const int v = tid + q * kSelThreads;
+      if (v < nvec) buf[q] = reinterpret_cast<const uint4*>(nrow)[v];
+    }
+#pragma unroll
+    for (int q = 0; q < MAXV; ++q) {
+      const int v = tid + q * kSelThreads;
+      if (v < nvec) {
+        const uint32_t w[4] = {buf[q].x, buf[q].y, buf[q].z, buf[q].w};
+        uint32_t kw[4], iw[4];
+        if constexpr (DT == KVC_BF16) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            kw[e] = (uint32_t)key_bf16(w[e] & 0xFFFFu, desc) |
+                    ((uint32_t)key_bf16(w[e] >> 16, desc) << 16);
+            iw[e] = (uint32_t)(v * 8 + 2 * e) | ((uint32_t)(v * 8 + 2 * e + 1) << 16);
+          }
+          *reinterpret_cast<uint4*>(key + v * 8) = make_uint4(kw[0], kw[1], kw[2], kw[3]);
+          *reinterpret_cast<uint4*>(idx + v * 8) = make_uint4(iw[0], iw[1], iw[2], iw[3]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) kw[e] = key_f32(w[e], desc);
+          *reinterpret_cast<uint4*>(key + v * 4) = make_uint4(kw[0], kw[1], kw[2], kw[3]);
+          *reinterpret_cast<uint2*>(idx + v * 4) =
+              make_uint2((uint32_t)(v * 4) | ((uint32_t)(v * 4 + 1) << 16),
+                         (uint32_t)(v * 4 + 2) | ((uint32_t)(v * 4 + 3) << 16));
+        }
+      }
     }
   }
   __syncthreads();
+  KVC_STAMP(1);
 
   // ---- reference-exact k-selection ----
   const bool topk = algo == KVC_ALGO_TOPK;
@@ -545,8 +589,10 @@ __global__ void __launch_bounds__(kSelThreads)
     }
     __syncthreads();
   }
+  KVC_STAMP(2);
   if (sc.state == 2 && wid == 0) wave_chain(key, idx, spos, k, topk, thr, sc.lo, sc.hi, sc.depth, sc);
   __syncthreads();
+  KVC_STAMP(3);
 
   // ---- emit the kept set {idx[0..k)} as ascending zone-local indices ----
   uint16_t* flag = spos;
@@ -574,6 +620,7 @@ __global__ void __launch_bounds__(kSelThreads)
     if (f) out[run + __popcll(bf & lanemask_lt(lane))] = wbeg + j * 64 + lane;
     run += __popcll(bf);
   }
+  KVC_STAMP(4);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -768,6 +815,9 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
     off = round_up(off + (size_t)rows * info->norm_row_stride * es, 256);
     info->index_offset = off;
     off = round_up(off + (size_t)rows * info->index_row_stride * 4, 256);
+#ifdef KVC_STAMPS
+    off += (size_t)rows * 64;  // diagnostic stamp slots (8 x u64 per select row)
+#endif
     info->workspace_bytes = off;
   }
   return KVC_OK;
@@ -869,6 +919,11 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
   int32_t* idx = reinterpret_cast<int32_t*>(w + info.index_offset);
   bool any_sel = false;
   for (int l = 0; l < nl; ++l) any_sel |= layers[l].n_select > 0;
+#ifdef KVC_STAMPS
+  uint64_t* stamps = reinterpret_cast<uint64_t*>(w + info.workspace_bytes - info.rows * 64);
+#else
+  uint64_t* stamps = nullptr;
+#endif
   (void)hipGetLastError();
   if ((p->phases & KVC_PHASE_SCORE) && info.score_tiles > 0 && !p->external_index) {
     if (p->dtype == KVC_BF16)
@@ -882,10 +937,10 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
     const dim3 grid((unsigned)info.rows), block(kSelThreads);
     if (p->dtype == KVC_BF16)
       hipLaunchKernelGGL(select_kernel<KVC_BF16>, grid, block, 0, s, layers_dev, BH, p->order,
-                         p->algo, norms, info.norm_row_stride, idx, info.index_row_stride);
+                         p->algo, norms, info.norm_row_stride, idx, info.index_row_stride, stamps);
     else
       hipLaunchKernelGGL(select_kernel<KVC_F32>, grid, block, 0, s, layers_dev, BH, p->order,
-                         p->algo, norms, info.norm_row_stride, idx, info.index_row_stride);
+                         p->algo, norms, info.norm_row_stride, idx, info.index_row_stride, stamps);
   }
   if ((p->phases & KVC_PHASE_GATHER) && info.gather_units > 0) {
     int64_t max_out = 0;

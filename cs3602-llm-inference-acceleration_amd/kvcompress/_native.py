@@ -10,6 +10,8 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_lib", "libkvc.so")
+# diagnostic builds (e.g. the s_memtime-stamped select kernel) may be swapped in by path
+LIB_PATH = os.environ.get("KVC_LIB", LIB_PATH)
 
 KVC_F32, KVC_BF16 = 0, 1
 KVC_ASC, KVC_DESC = 0, 1

@@ -24,3 +24,7 @@ if [ "$MODE" = "micro" ]; then
   timeout -k 10 300 python tools/microbench.py "${2:-lds,direct}" "${3:-5}" > gpurun_out/micro.json 2> gpurun_out/micro.err || exit $?
   cat gpurun_out/micro.json
 fi
+if [ "$MODE" = "stamps" ]; then
+  timeout -k 10 300 python tools/select_stamps.py > gpurun_out/stamps.json 2> gpurun_out/stamps.err || exit $?
+  cat gpurun_out/stamps.json
+fi

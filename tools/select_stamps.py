@@ -1,0 +1,52 @@
+"""Phase breakdown of the select kernel from the diagnostic stamps build (libkvc_stamps.so):
+median per-row cycles of key load / block chain / wave chain / emission on the headline
+workload (32 layers x 32 heads, S=16384, k=512).  GPU box only; read shares, not absolutes."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["KVC_LIB"] = os.path.join(ROOT, "cs3602-llm-inference-acceleration_amd", "kvcompress",
+                                     "_lib", "libkvc_stamps.so")
+sys.path.insert(0, os.path.join(ROOT, "cs3602-llm-inference-acceleration_amd"))
+from kvcompress import _native as N  # noqa: E402
+
+dev = torch.device("cuda:0")
+g = torch.Generator(device=dev).manual_seed(0)
+L, H, S, D, k = 32, 32, 16384, 128, 512
+Ks = [torch.randn(1, H, S, D, device=dev, generator=g).to(torch.bfloat16) for _ in range(L)]
+table = np.zeros(L, dtype=N.LAYER_DTYPE)
+outs = []
+for i, K in enumerate(Ks):
+    o = torch.empty(1, H, k, D, dtype=K.dtype, device=dev)
+    outs.append(o)
+    t = table[i]
+    t["k"] = t["v"] = K.data_ptr()
+    t["k_out"] = t["v_out"] = o.data_ptr()
+    t["k_stride"] = t["v_stride"] = K.stride()[:3]
+    t["seq_len"], t["zone_start"], t["zone_len"], t["n_select"] = S, 0, S, k
+p = N.Params(dtype=N.KVC_BF16, batch=1, heads=H, head_dim=D, order=0, algo=0,
+             phases=N.PHASE_SCORE | N.PHASE_SELECT, external_index=0)
+rc, info = N.plan(p, table)
+assert rc == 0
+ws = torch.zeros(int(info.workspace_bytes), dtype=torch.uint8, device=dev)
+res = {}
+for rep in range(3):
+    rc = N.launch(p, table, 0, ws.data_ptr(), int(info.workspace_bytes),
+                  torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+rows = int(info.rows)
+st = ws[-rows * 64:].view(torch.int64).view(rows, 8).cpu().numpy()[:, :5].astype(np.float64)
+d = np.diff(st, axis=1)
+names = ["key_load", "block_chain", "wave_chain", "emit"]
+res["median_cycles"] = {n: float(np.median(d[:, i])) for i, n in enumerate(names)}
+res["p90_cycles"] = {n: float(np.percentile(d[:, i], 90)) for i, n in enumerate(names)}
+res["row_total_median"] = float(np.median(st[:, 4] - st[:, 0]))
+res["span_cycles"] = float(st[:, 4].max() - st[:, 0].min())
+starts = np.sort(st[:, 0] - st[:, 0].min())
+res["start_quantiles"] = [float(x) for x in np.percentile(starts, [0, 25, 50, 75, 100])]
+print(json.dumps(res))
