@@ -200,10 +200,10 @@ __global__ void __launch_bounds__(kScoreThreads)
 // ---------------------------------------------------------------------------------------------
 template <typename KeyT>
 struct SelScalars {
-  int m[2];      // swap count of the current partition (double-buffered by level parity)
-  int gnext[2];  // g_{m+1}: first "not less than pivot" position that is not swapped
-  int wtot[kSelWaves];
+  int lo, hi, state, m, gnext, depth;
+  KeyT p;
   int wa[kSelWaves];
+  int wb[kSelWaves];
   float fmax[kSelWaves];
   int fnan[kSelWaves];
 };
@@ -274,43 +274,32 @@ __device__ void snapkv_keys(const char* nrow, int n, int pool_k, bool desc, KeyT
   }
 }
 
-template <int NT>
-__device__ __forceinline__ void group_sync() {
-  if constexpr (NT == 64)
-    wave_sync();
-  else
-    __syncthreads();
-}
-
-// The partition chain of libstdc++ introsort (topk = false) / introselect (topk = true),
-// following only the segment [lo, hi) that straddles position k, run by NT cooperating lanes
-// (the whole 1024-thread block, or one wave for short segments).  One level is one
-// std::__move_median_to_first + std::__unguarded_partition(lo+1, hi, lo), computed in parallel:
-//   g_t = t-th position (ascending) in [lo+1,hi) with !(key < p)          ("ge")
-//   s_t = t-th position (descending) with !(p < key), then the pivot slot lo ("le")
-// libstdc++ swaps g_t <-> s_t for every t with g_t < s_t -- a prefix t <= m -- and returns
-// cut = min(g_{m+1}, s_m).  With A(x) = #ge before x and Lin(x) = #le in [lo+1, x]:
-//   g_t < s_t  <=>  A(g_t) + Lin(g_t) < tot_le,
-// so m is a count over ge positions and only s needs a rank -> position table (spos).
-// Each lane owns a contiguous, 16-byte aligned chunk of <= 32 positions (ds_read_b128 loads).
-// Returns 0 when the first-k set is final, 1 when a block hands a short segment to one wave.
-template <typename KeyT, int NT>
-__device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, SelScalars<KeyT>& sc, int k,
-                         bool topk, int thr, int& lo, int& hi, int& depth, int& level) {
-  constexpr int VK = 16 / (int)sizeof(KeyT);
-  const int tid = (NT == 64) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+// The rest of the partition chain once the straddling segment is <= kWaveSeg long, run by one
+// wave (64 lanes x <= 16 positions) with wave-level synchronisation only.  Same algorithm as the
+// block-level loop in select_kernel; lo/hi/depth are uniform across the wave's lanes.
+template <typename KeyT>
+__device__ void wave_chain(KeyT* key, uint16_t* idx, uint16_t* spos, int k, bool topk, int thr,
+                           int lo, int hi, int depth, SelScalars<KeyT>& sc) {
   const int lane = threadIdx.x & 63;
-  const int wid = (NT == 64) ? 0 : (int)(threadIdx.x >> 6);
+  int msw = 0, gnext = kBig;
+  bool first = true;
   while (true) {
-    if (lo == k || hi == k) return 0;  // a partition boundary sits at k: the set is final
-    if (hi - lo <= thr) {              // final (stable) insertion sort of the segment
-      if (tid == 0) insertion_sort(key, idx, lo, hi);
-      group_sync<NT>();
-      return 0;
+    if (!first) {
+      const int cut = min(gnext, msw > 0 ? (int)spos[msw] : kBig);
+      if (topk) {
+        if (cut <= k - 1) lo = cut; else hi = cut;
+      } else {
+        if (k <= cut) hi = cut; else lo = cut;
+      }
     }
-    if (NT > 64 && hi - lo <= kWaveSeg) return 1;
-    if (depth == 0) {  // depth limit: libstdc++ switches to heap algorithms
-      if (tid == 0) {
+    first = false;
+    if (lo == k || hi == k) break;
+    if (hi - lo <= thr) {
+      if (lane == 0) insertion_sort(key, idx, lo, hi);
+      break;
+    }
+    if (depth == 0) {
+      if (lane == 0) {
         if (topk) {
           heap_select(key + lo, idx + lo, k - lo, hi - lo);
           kv_swap(key, idx, lo, k - 1);
@@ -319,126 +308,68 @@ __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, SelScalars<Ke
           sort_heap(key + lo, idx + lo, hi - lo);
         }
       }
-      group_sync<NT>();
-      return 0;
+      break;
     }
     --depth;
-    const int par = level & 1;
-    // ---- median of three (every lane, redundantly); the swap into lo is virtual until P2 ----
-    const int a = lo + 1, b = lo + (hi - lo) / 2, c = hi - 1;
-    const KeyT ka = key[a], kb = key[b], kc = key[c], klo = key[lo];
-    int ch;
-    if (ka < kb) {
-      if (kb < kc) ch = b; else if (ka < kc) ch = c; else ch = a;
-    } else if (ka < kc) {
-      ch = a;
-    } else if (kb < kc) {
-      ch = c;
-    } else {
-      ch = b;
-    }
-    const KeyT p = (ch == a) ? ka : (ch == b) ? kb : kc;
-    // ---- P1: flags of this lane's chunk ----
-    const int base = (lo + 1) & ~(VK - 1);
-    int E = (hi - base + NT - 1) / NT;
-    E = (E + VK - 1) / VK * VK;
-    const int c0 = base + tid * E;
-    uint32_t gem = 0, lem = 0;
-    for (int v = 0; v < E; v += VK) {
-      const int p0 = c0 + v;
-      if (p0 >= hi) break;
-      const uint4 w = *reinterpret_cast<const uint4*>(key + p0);
-      const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-      for (int e = 0; e < VK; ++e) {
-        KeyT kk;
-        if constexpr (sizeof(KeyT) == 2)
-          kk = (KeyT)((ws[e >> 1] >> (16 * (e & 1))) & 0xFFFFu);
-        else
-          kk = (KeyT)ws[e];
-        const int pos = p0 + e;
-        if (pos == ch) kk = klo;
-        const bool valid = pos > lo && pos < hi;
-        gem |= (uint32_t)(valid && !(kk < p)) << (v + e);
-        lem |= (uint32_t)(valid && !(p < kk)) << (v + e);
-      }
-    }
-    const uint32_t cnt = (uint32_t)__popc(gem) | ((uint32_t)__popc(lem) << 16);
-    uint32_t x = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o, 64);
-      if (lane >= o) x += y;
-    }
-    uint32_t before = 0, tot;
-    if constexpr (NT == 64) {
-      tot = __shfl(x, 63, 64);
-    } else {
-      if (lane == 63) sc.wtot[wid] = (int)x;
-      __syncthreads();  // B_a
-      tot = 0;
-#pragma unroll
-      for (int w2 = 0; w2 < NT / 64; ++w2) {
-        const uint32_t t2 = (uint32_t)sc.wtot[w2];
-        before += (w2 < wid) ? t2 : 0u;
-        tot += t2;
-      }
-    }
-    const uint32_t excl = before + x - cnt;
-    const int ge_excl = (int)(excl & 0xFFFFu), le_excl = (int)(excl >> 16);
-    const int tot_le = (int)(tot >> 16);
-    // ---- P2: s rank table, swap count, g_{m+1} ----
-    if (tid == 0) {
-      kv_swap(key, idx, lo, ch);  // std::__move_median_to_first, made physical
-      spos[tot_le + 1] = (uint16_t)lo;
-      sc.m[par ^ 1] = 0;
-      sc.gnext[par ^ 1] = kBig;
-    }
-    int nsw = 0, first_false = kBig;
-    for (int j = 0; j < E; ++j) {
-      const uint32_t bit = 1u << j;
-      if (!((gem | lem) & bit)) continue;
-      const int pos = c0 + j;
-      const int lin = le_excl + __popc(lem & (bit | (bit - 1u)));
-      if (lem & bit) spos[tot_le - lin + 1] = (uint16_t)pos;
-      if (gem & bit) {
-        const int A = ge_excl + __popc(gem & (bit - 1u));
-        if (A + lin < tot_le)
-          ++nsw;
-        else if (first_false == kBig)
-          first_false = pos;
-      }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      nsw += __shfl_xor(nsw, o, 64);
-      first_false = min(first_false, __shfl_xor(first_false, o, 64));
-    }
     if (lane == 0) {
-      if (nsw) atomicAdd(&sc.m[par], nsw);
-      if (first_false != kBig) atomicMin(&sc.gnext[par], first_false);
+      move_median_to_first(key, idx, lo, lo + 1, lo + (hi - lo) / 2, hi - 1);
+      sc.gnext = kBig;
     }
-    group_sync<NT>();  // B_b
-    // ---- P4: the m swaps (disjoint pairs) ----
-    const int msw = sc.m[par];
-    if (ge_excl < msw) {
-      for (int j = 0; j < E; ++j) {
-        const uint32_t bit = 1u << j;
-        if (!(gem & bit)) continue;
-        const int t = ge_excl + __popc(gem & (bit - 1u)) + 1;
-        if (t > msw) break;
-        kv_swap(key, idx, c0 + j, (int)spos[t]);
+    wave_sync();
+    const KeyT p = key[lo];
+    const int J = (hi - lo - 1 + 63) / 64;  // <= 16
+    uint32_t gem = 0, lem = 0;
+    int tot_le = 0;
+    for (int j = 0; j < J; ++j) {
+      const int pos = lo + 1 + j * 64 + lane;
+      const bool valid = pos < hi;
+      const KeyT kk = valid ? key[pos] : (KeyT)0;
+      const bool ge = valid && !(kk < p);
+      const bool le = valid && !(p < kk);
+      gem |= (uint32_t)ge << j;
+      lem |= (uint32_t)le << j;
+      tot_le += __popcll(__ballot(le));
+    }
+    int run = 0;
+    for (int j = 0; j < J; ++j) {
+      const bool le = (lem >> j) & 1u;
+      const uint64_t bl = __ballot(le);
+      if (le) {
+        const int incl = run + __popcll(bl & lanemask_le(lane));
+        spos[tot_le - incl + 1] = (uint16_t)(lo + 1 + j * 64 + lane);
       }
+      run += __popcll(bl);
     }
-    group_sync<NT>();  // B_c
-    const int cut = min(sc.gnext[par], msw > 0 ? (int)spos[msw] : kBig);
-    if (topk) {  // std::__introselect: if (cut <= nth) first = cut; else last = cut;
-      if (cut <= k - 1) lo = cut; else hi = cut;
-    } else {     // std::__introsort_loop: recurse right, loop on the left part
-      if (k <= cut) hi = cut; else lo = cut;
+    if (lane == 0) spos[tot_le + 1] = (uint16_t)lo;
+    wave_sync();
+    run = 0;
+    msw = 0;
+    for (int j = 0; j < J; ++j) {
+      const bool ge = (gem >> j) & 1u;
+      const uint64_t bg = __ballot(ge);
+      const int t = run + __popcll(bg & lanemask_lt(lane)) + 1;
+      const bool pair = ge && t <= tot_le + 1 && (int)spos[t] > lo + 1 + j * 64 + lane;
+      msw += __popcll(__ballot(pair));
+      run += __popcll(bg);
     }
-    ++level;
+    run = 0;
+    for (int j = 0; j < J; ++j) {
+      const bool ge = (gem >> j) & 1u;
+      const uint64_t bg = __ballot(ge);
+      if (ge) {
+        const int t = run + __popcll(bg & lanemask_lt(lane)) + 1;
+        const int pos = lo + 1 + j * 64 + lane;
+        if (t <= msw)
+          kv_swap(key, idx, pos, (int)spos[t]);
+        else if (t == msw + 1)
+          sc.gnext = pos;
+      }
+      run += __popcll(bg);
+    }
+    wave_sync();
+    gnext = sc.gnext;
   }
+  wave_sync();
 }
 
 template <int DT>
@@ -518,10 +449,6 @@ __global__ void __launch_bounds__(kSelThreads)
       }
     }
   }
-  if (tid == 0) {
-    sc.m[0] = 0;
-    sc.gnext[0] = kBig;
-  }
   __syncthreads();
   KVC_STAMP(1);
 
@@ -529,16 +456,141 @@ __global__ void __launch_bounds__(kSelThreads)
   const bool topk = algo == KVC_ALGO_TOPK;
   const bool partial = topk && (int64_t)k * 64 <= n;  // aten TopKImpl.h: use_partial_sort
   const int thr = topk ? 3 : 16;  // introselect / introsort segment threshold
-  if (partial) {
-    if (tid == 0) heap_select(key, idx, k, n);  // std::partial_sort's heap select
-  } else {
-    int lo = 0, hi = n, depth = 2 * floor_log2(n), level = 0;
-    const int st = run_chain<KeyT, kSelThreads>(key, idx, spos, sc, k, topk, thr, lo, hi, depth,
-                                                level);
-    KVC_STAMP(2);
-    if (st == 1 && wid == 0)
-      run_chain<KeyT, 64>(key, idx, spos, sc, k, topk, thr, lo, hi, depth, level);
+  int lo = 0, hi = n, depth = 2 * floor_log2(n);  // chain state, owned by thread 0
+  bool first = true;
+  while (true) {
+    if (tid == 0) {
+      int state = 1;
+      if (partial) {
+        heap_select(key, idx, k, n);  // std::partial_sort's heap select; set = first k
+      } else {
+        if (!first) {  // finish the previous partition: cut = min(g_{m+1}, s_m)
+          const int cut = min(sc.gnext, sc.m > 0 ? (int)spos[sc.m] : kBig);
+          if (topk) {  // std::__introselect: if (cut <= nth) first = cut; else last = cut;
+            if (cut <= k - 1) lo = cut; else hi = cut;
+          } else {     // std::__introsort_loop: right part recursed, loop on the left
+            if (k <= cut) hi = cut; else lo = cut;
+          }
+        }
+        if (lo == k || hi == k) {
+          // a partition boundary sits exactly at k: the first-k set is final
+        } else if (hi - lo <= kWaveSeg) {
+          state = 2;  // short segment: wave 0 finishes the chain without block barriers
+          sc.lo = lo;
+          sc.hi = hi;
+          sc.depth = depth;
+        } else if (depth == 0) {  // depth limit: libstdc++ switches to heap algorithms
+          if (topk) {
+            heap_select(key + lo, idx + lo, k - lo, hi - lo);
+            kv_swap(key, idx, lo, k - 1);
+          } else {
+            make_heap(key + lo, idx + lo, hi - lo);
+            sort_heap(key + lo, idx + lo, hi - lo);
+          }
+        } else {
+          --depth;
+          move_median_to_first(key, idx, lo, lo + 1, lo + (hi - lo) / 2, hi - 1);
+          sc.p = key[lo];
+          sc.lo = lo;
+          sc.hi = hi;
+          sc.m = 0;
+          sc.gnext = kBig;
+          state = 0;
+        }
+      }
+      sc.state = state;
+    }
+    first = false;
+    __syncthreads();
+    if (sc.state) break;
+
+    // ---- one std::__unguarded_partition(lo+1, hi, pivot=lo), computed in parallel ----
+    // g_t: t-th position (ascending) in [lo+1,hi) with !(key < p); s_t: t-th position
+    // (descending) with !(p < key), followed by the pivot slot lo.  libstdc++ swaps g_t<->s_t
+    // for every t with g_t < s_t (a prefix of t) and returns min(g_{m+1}, s_m).
+    const int plo = sc.lo, phi = sc.hi;
+    const KeyT p = sc.p;
+    const int m1 = phi - plo - 1;
+    const int J = (m1 + kSelThreads - 1) / kSelThreads;  // <= 16 positions per lane
+    const int wbeg = plo + 1 + wid * J * 64;
+    uint32_t gem = 0, lem = 0;
+    int cge = 0, cle = 0;
+    for (int j = 0; j < J; ++j) {
+      const int pos = wbeg + j * 64 + lane;
+      const bool valid = pos < phi;
+      const KeyT kk = valid ? key[pos] : (KeyT)0;
+      const bool ge = valid && !(kk < p);
+      const bool le = valid && !(p < kk);
+      gem |= (uint32_t)ge << j;
+      lem |= (uint32_t)le << j;
+      cge += __popcll(__ballot(ge));
+      cle += __popcll(__ballot(le));
+    }
+    if (lane == 0) {
+      sc.wa[wid] = cge;
+      sc.wb[wid] = cle;
+    }
+    __syncthreads();
+    int ge_before = 0, le_before = 0, tot_le = 0;
+    for (int w = 0; w < kSelWaves; ++w) {
+      const int a = sc.wa[w], bb = sc.wb[w];
+      if (w < wid) {
+        ge_before += a;
+        le_before += bb;
+      }
+      tot_le += bb;
+    }
+    {  // s positions by descending rank (1-based); the pivot slot closes the list
+      int run = le_before;
+      for (int j = 0; j < J; ++j) {
+        const bool le = (lem >> j) & 1u;
+        const uint64_t bl = __ballot(le);
+        if (le) {
+          const int incl = run + __popcll(bl & lanemask_le(lane));
+          spos[tot_le - incl + 1] = (uint16_t)(wbeg + j * 64 + lane);
+        }
+        run += __popcll(bl);
+      }
+      if (tid == 0) spos[tot_le + 1] = (uint16_t)plo;
+    }
+    __syncthreads();
+    {  // number of swaps m = #{t : g_t < s_t}
+      int run = ge_before, cnt = 0;
+      for (int j = 0; j < J; ++j) {
+        const bool ge = (gem >> j) & 1u;
+        const uint64_t bg = __ballot(ge);
+        if (ge) {
+          const int t = run + __popcll(bg & lanemask_lt(lane)) + 1;
+          if (t <= tot_le + 1 && (int)spos[t] > wbeg + j * 64 + lane) ++cnt;
+        }
+        run += __popcll(bg);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+      if (lane == 0 && cnt) atomicAdd(&sc.m, cnt);
+    }
+    __syncthreads();
+    {  // the swaps (all pairs are disjoint) and g_{m+1}
+      const int msw = sc.m;
+      int run = ge_before;
+      for (int j = 0; j < J; ++j) {
+        const bool ge = (gem >> j) & 1u;
+        const uint64_t bg = __ballot(ge);
+        if (ge) {
+          const int t = run + __popcll(bg & lanemask_lt(lane)) + 1;
+          const int pos = wbeg + j * 64 + lane;
+          if (t <= msw)
+            kv_swap(key, idx, pos, (int)spos[t]);
+          else if (t == msw + 1)
+            sc.gnext = pos;
+        }
+        run += __popcll(bg);
+      }
+    }
+    __syncthreads();
   }
+  KVC_STAMP(2);
+  if (sc.state == 2 && wid == 0) wave_chain(key, idx, spos, k, topk, thr, sc.lo, sc.hi, sc.depth, sc);
   __syncthreads();
   KVC_STAMP(3);
 

@@ -6,6 +6,7 @@ arithmetic) and, for every layer that the reference would gather/concatenate, re
 batched engine launch per (device, dtype, batch, heads, head_dim) group -- score, select and
 gather kernels over every layer at once -- and writes the new (K, V) tensors back into the list.
 """
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -101,13 +102,72 @@ def execute(jobs: List[Segments], out_list: list, order: int, algo: int):
         _run_group(device, dtype, B, H, D, js, out_list, order, algo)
 
 
+def _pipeline_chunks(n_layers, external):
+    """Layer chunks for the score/select pipeline (KVC_PIPELINE_CHUNKS overrides; 1 = serial)."""
+    env = os.environ.get("KVC_PIPELINE_CHUNKS")
+    c = int(env) if env else (4 if n_layers >= 8 else 1)
+    if external or n_layers < 2:
+        return 1
+    return max(1, min(c, n_layers))
+
+
+_side_streams = {}
+
+
+def _side_stream(device):
+    s = _side_streams.get(device)
+    if s is None:
+        s = _side_streams[device] = torch.cuda.Stream(device=device)
+    return s
+
+
+def _upload(params, table, device, js, B, H):
+    """Plan one table, allocate its workspace and enqueue the descriptor upload (current stream)."""
+    rc, info = N.plan(params, table)
+    N.check(rc, "kvc_plan")
+    ws = torch.empty(max(int(info.workspace_bytes), 256), dtype=torch.uint8, device=device)
+    tbl = torch.from_numpy(table.view(np.uint8)).pin_memory()
+    ws[info.desc_offset:info.desc_offset + tbl.numel()].copy_(tbl, non_blocking=True)
+    if params.external_index:
+        istride = int(info.index_row_stride)
+        iv = ws[info.index_offset:info.index_offset + int(info.rows) * istride * 4]
+        iv = iv.view(torch.int32).view(int(info.rows), istride)
+        for i, j in enumerate(js):
+            if j.n_select:
+                iv[i * B * H:(i + 1) * B * H, :j.n_select].copy_(
+                    j.ext_index.reshape(B * H, j.n_select))
+    return ws, info
+
+
+def _launch(params, table, ws, info, stream, phases):
+    dev_tbl = ws.data_ptr() + int(info.desc_offset)
+    saved = params.phases
+    steps = ((("score", N.PHASE_SCORE), ("select", N.PHASE_SELECT), ("gather", N.PHASE_GATHER))
+             if _timer is not None else (("all", phases),))
+    for name, bits in steps:
+        if not phases & bits:
+            continue
+        params.phases = bits
+        if _timer is not None:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+        rc = N.launch(params, table, dev_tbl, ws.data_ptr(), int(info.workspace_bytes),
+                      stream.cuda_stream)
+        if _timer is not None:
+            b.record(stream)
+        N.check(rc, "kvc_launch")
+        if _timer is not None:
+            _timer.records.append((name, a, b))
+    params.phases = saved
+
+
 def _run_group(device, dtype, B, H, D, js, out_list, order, algo):
     n = len(js)
     external = any(j.ext_index is not None for j in js)
     if external and not all(j.ext_index is not None or j.n_select == 0 for j in js):
         raise RuntimeError("mixed external / engine-selected layers in one group")
     table = np.zeros(n, dtype=N.LAYER_DTYPE)
-    keep = []  # keep prepared inputs alive until the launch is enqueued
+    keep = []  # prepared (possibly contiguous-copied) inputs stay alive until enqueued
     outs = []
     for i, j in enumerate(js):
         k, v = _prep(j.keys), _prep(j.values)
@@ -125,42 +185,39 @@ def _run_group(device, dtype, B, H, D, js, out_list, order, algo):
         t["zone_start"], t["zone_len"], t["n_select"] = j.zone_start, j.zone_len, j.n_select
         t["sink_len"], t["tail_start"], t["tail_len"] = j.sink_len, j.tail_start, j.tail_len
         t["pool_kernel"], t["score_mode"] = j.pool_kernel, j.score_mode
-    params = N.Params(dtype=_SUPPORTED[dtype], batch=B, heads=H, head_dim=D, order=order,
-                      algo=algo, phases=N.PHASE_GATHER if external else N.PHASE_ALL,
-                      external_index=1 if external else 0)
-    rc, info = N.plan(params, table)
-    N.check(rc, "kvc_plan")
+
+    def params():
+        return N.Params(dtype=_SUPPORTED[dtype], batch=B, heads=H, head_dim=D, order=order,
+                        algo=algo, phases=N.PHASE_GATHER if external else N.PHASE_ALL,
+                        external_index=1 if external else 0)
+
+    C = _pipeline_chunks(n, external)
+    bounds = [n * c // C for c in range(C + 1)]
     with torch.cuda.device(device):
-        ws = torch.empty(max(int(info.workspace_bytes), 256), dtype=torch.uint8, device=device)
-        tbl = torch.from_numpy(table.view(np.uint8)).pin_memory()
-        ws[info.desc_offset:info.desc_offset + tbl.numel()].copy_(tbl, non_blocking=True)
-        if external:
-            istride = int(info.index_row_stride)
-            iv = ws[info.index_offset:info.index_offset + int(info.rows) * istride * 4]
-            iv = iv.view(torch.int32).view(int(info.rows), istride)
-            for i, j in enumerate(js):
-                if j.n_select:
-                    iv[i * B * H:(i + 1) * B * H, :j.n_select].copy_(
-                        j.ext_index.reshape(B * H, j.n_select))
-        stream = torch.cuda.current_stream(device).cuda_stream
-        dev_tbl = ws.data_ptr() + int(info.desc_offset)
-        if _timer is None:
-            rc = N.launch(params, table, dev_tbl, ws.data_ptr(), int(info.workspace_bytes), stream)
-            N.check(rc, "kvc_launch")
+        main = torch.cuda.current_stream(device)
+        chunks = []
+        for c in range(C):
+            sub = table[bounds[c]:bounds[c + 1]].copy()
+            p = params()
+            ws, info = _upload(p, sub, device, js[bounds[c]:bounds[c + 1]], B, H)
+            chunks.append((p, sub, ws, info))
+        if C == 1:
+            p, sub, ws, info = chunks[0]
+            _launch(p, sub, ws, info, main, p.phases)
         else:
-            phases = params.phases
-            for name, bit in (("score", N.PHASE_SCORE), ("select", N.PHASE_SELECT),
-                              ("gather", N.PHASE_GATHER)):
-                if not phases & bit:
-                    continue
-                params.phases = bit
-                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a.record()
-                rc = N.launch(params, table, dev_tbl, ws.data_ptr(), int(info.workspace_bytes),
-                              stream)
-                b.record()
-                N.check(rc, "kvc_launch")
-                _timer.records.append((name, a, b))
-            params.phases = phases
+            # score chunk c+1 on a side stream while chunk c selects/gathers on the caller's
+            # stream; the caller's stream waits for every score event, so all side-stream work
+            # is complete (stream-ordered) before anything later on the caller's stream runs.
+            side = _side_stream(device)
+            side.wait_stream(main)
+            events = []
+            for p, sub, ws, info in chunks:
+                _launch(p, sub, ws, info, side, N.PHASE_SCORE)
+                ev = torch.cuda.Event()
+                ev.record(side)
+                events.append(ev)
+            for (p, sub, ws, info), ev in zip(chunks, events):
+                main.wait_event(ev)
+                _launch(p, sub, ws, info, main, N.PHASE_SELECT | N.PHASE_GATHER)
     for j, (ko, vo) in zip(js, outs):
         out_list[j.layer_idx] = (ko, vo)

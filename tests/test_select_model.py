@@ -34,8 +34,6 @@ def model():
     for f in ("model_key_bf16", "model_key_f32", "model_canon_nan"):
         getattr(L, f).restype = ctypes.c_uint32
         getattr(L, f).argtypes = [ctypes.c_uint32, ctypes.c_int] if "key" in f else [ctypes.c_uint32]
-    L.model_select_v2.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                  ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
     L.model_f32_to_bf16.restype = ctypes.c_uint32
     L.model_f32_to_bf16.argtypes = [ctypes.c_float]
     return L
@@ -134,41 +132,3 @@ def test_bf16_rounding_and_nan_canonicalisation(model):
             return 0xFFFF if (h & 0x7FFF) > 0x7F80 else h
         assert model.model_canon_nan(w) == (c(lo) | (c(hi) << 16))
 
-
-def run_model_v2(L, keys_u32, k, topk, key16):
-    keys_u32 = np.ascontiguousarray(keys_u32, dtype=np.uint32)
-    out = np.empty(max(k, 1), dtype=np.int32)
-    path = ctypes.c_int(0)
-    rc = L.model_select_v2(keys_u32.ctypes.data, len(keys_u32), k, topk, key16, out.ctypes.data,
-                           ctypes.byref(path))
-    assert rc == 0
-    return out[:k], path.value
-
-
-def test_parallel_formulation_matches_libstdcxx(model):
-    """The lane-parallel partition formulation run_chain uses (mirrored lane by lane)."""
-    rng = np.random.default_rng(4)
-    for trial in range(600):
-        n = int(rng.integers(2, 16385)) if trial % 3 else int(rng.integers(2, 3000))
-        hi_val = int(rng.choice([1, 2, 3, 7, 80, 1 << 15]))
-        keys = rng.integers(0, hi_val, n).astype(np.uint32)
-        k = int(rng.integers(1, n))
-        for topk in (0, 1):
-            for key16 in (1, 0):
-                got, _ = run_model_v2(model, keys, k, topk, key16)
-                np.testing.assert_array_equal(got, ref_set(keys, k, topk),
-                                              err_msg=f"n={n} k={k} topk={topk} key16={key16}")
-
-
-@pytest.mark.parametrize("n", [1000, 4096, 16384])
-def test_parallel_formulation_adversarial(model, n):
-    adv = np.empty(n, dtype=np.int64)
-    hit = 0
-    for mode in (0, 1):
-        for k in (1, n // 3, n // 2, n - 1):
-            oracle.lib().orc_antiqsort(n, mode, k, adv.ctypes.data)
-            keys = adv.astype(np.uint32)
-            got, path = run_model_v2(model, keys, k, mode, 1 if n <= 65535 else 0)
-            hit += path == 2
-            np.testing.assert_array_equal(got, ref_set(keys, k, mode))
-    assert hit > 0

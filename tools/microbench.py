@@ -11,7 +11,8 @@ sys.path.insert(0, os.path.join(ROOT, "cs3602-llm-inference-acceleration_amd"))
 from kvcompress import _engine  # noqa: E402
 from kvcompress.methods import fix_size_l2_compress  # noqa: E402
 
-variants = sys.argv[1].split(",") if len(sys.argv) > 1 else ["lds", "direct"]
+# variant = "<score kernel>:<pipeline chunks>", e.g. lds:1,lds:4
+variants = sys.argv[1].split(",") if len(sys.argv) > 1 else ["lds:1", "lds:4"]
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(0)
@@ -22,13 +23,21 @@ res = {v: {} for v in variants}
 ref = None
 for r in range(rounds):
     for v in variants:
-        os.environ["KVC_SCORE_VARIANT"] = v
+        kern, chunks = (v.split(":") + ["1"])[:2]
+        os.environ["KVC_SCORE_VARIANT"] = kern
+        os.environ["KVC_PIPELINE_CHUNKS"] = chunks
         t = _engine.PhaseTimer()
         _engine.set_phase_timer(t)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
         for _ in range(5):
             out = fix_size_l2_compress(layers, fix_kv_size=512, skip_layers=[])
+        b.record()
         _engine.set_phase_timer(None)
         d = t.durations_ms()
+        d = {ph: [sum(xs) / 5] for ph, xs in d.items()}  # per-step kernel time (all chunks)
+        d["step_wall"] = [a.elapsed_time(b) / 5]
         for ph, xs in d.items():
             res[v].setdefault(ph, []).append(min(xs))
         if ref is None:
