@@ -200,8 +200,8 @@ __global__ void __launch_bounds__(kScoreThreads)
 // ---------------------------------------------------------------------------------------------
 template <typename KeyT>
 struct SelScalars {
-  int lo, hi, state, m, gnext, depth;
-  KeyT p;
+  int m[2];      // swap count of the current partition (double-buffered by level parity)
+  int gnext[2];  // g_{m+1}: first "not less than pivot" position that is not swapped
   int wa[kSelWaves];
   int wb[kSelWaves];
   float fmax[kSelWaves];
@@ -274,32 +274,48 @@ __device__ void snapkv_keys(const char* nrow, int n, int pool_k, bool desc, KeyT
   }
 }
 
-// The rest of the partition chain once the straddling segment is <= kWaveSeg long, run by one
-// wave (64 lanes x <= 16 positions) with wave-level synchronisation only.  Same algorithm as the
-// block-level loop in select_kernel; lo/hi/depth are uniform across the wave's lanes.
-template <typename KeyT>
-__device__ void wave_chain(KeyT* key, uint16_t* idx, uint16_t* spos, int k, bool topk, int thr,
-                           int lo, int hi, int depth, SelScalars<KeyT>& sc) {
+template <int NT>
+__device__ __forceinline__ void group_sync() {
+  if constexpr (NT == 64)
+    wave_sync();
+  else
+    __syncthreads();
+}
+
+// The partition chain of libstdc++ introsort (topk = false) / introselect (topk = true),
+// following only the segment [lo, hi) that straddles position k, run by NT cooperating lanes
+// (the whole 1024-thread block, or one wave once the segment is short).  One level is
+// std::__move_median_to_first + std::__unguarded_partition(lo+1, hi, pivot=lo) computed in
+// parallel:
+//   g_t = t-th position (ascending) in [lo+1,hi) with !(key < p)            ("ge")
+//   s_t = t-th position (descending) with !(p < key), then the pivot slot lo ("le")
+// libstdc++ swaps g_t <-> s_t for every t with g_t < s_t -- a prefix t <= m -- and returns
+// cut = min(g_{m+1}, s_m).  With A(x) = #ge before x and Lin(x) = #le in [lo+1, x]:
+//   g_t < s_t  <=>  A(g_t) + Lin(g_t) < tot_le
+// (tests/native/select_model.cpp validates the chain against libstdc++), so m is counted in
+// the same pass that scatters the s rank -> position table.  Positions are laid out j-major
+// (lane + 64*j within a wave's stripe) so ge/le flags are wave ballots; every j-loop is fully
+// unrolled and loads are issued before dependent stores, keeping LDS latency off the chain.
+// Returns 0 when the first-k set is final, 1 when the block hands a short segment to one wave.
+template <typename KeyT, int NT>
+__device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, SelScalars<KeyT>& sc, int k,
+                         bool topk, int thr, int& lo, int& hi, int& depth, int& level) {
+  constexpr int NW = NT / 64;
+  constexpr int JM = 16;  // positions per lane: n <= 16384 at NT = 1024, m <= 1024 at NT = 64
   const int lane = threadIdx.x & 63;
-  int msw = 0, gnext = kBig;
-  bool first = true;
+  const int wid = (NT == 64) ? 0 : (int)(threadIdx.x >> 6);
+  const int tid = wid * 64 + lane;
+  const uint64_t lt = lanemask_lt(lane), le_m = lanemask_le(lane);
   while (true) {
-    if (!first) {
-      const int cut = min(gnext, msw > 0 ? (int)spos[msw] : kBig);
-      if (topk) {
-        if (cut <= k - 1) lo = cut; else hi = cut;
-      } else {
-        if (k <= cut) hi = cut; else lo = cut;
-      }
+    if (lo == k || hi == k) return 0;  // a partition boundary sits at k: the set is final
+    if (hi - lo <= thr) {              // final (stable) insertion sort of the segment
+      if (tid == 0) insertion_sort(key, idx, lo, hi);
+      group_sync<NT>();
+      return 0;
     }
-    first = false;
-    if (lo == k || hi == k) break;
-    if (hi - lo <= thr) {
-      if (lane == 0) insertion_sort(key, idx, lo, hi);
-      break;
-    }
-    if (depth == 0) {
-      if (lane == 0) {
+    if (NT > 64 && hi - lo <= kWaveSeg) return 1;
+    if (depth == 0) {  // depth limit: libstdc++ switches to heap algorithms
+      if (tid == 0) {
         if (topk) {
           heap_select(key + lo, idx + lo, k - lo, hi - lo);
           kv_swap(key, idx, lo, k - 1);
@@ -308,68 +324,159 @@ __device__ void wave_chain(KeyT* key, uint16_t* idx, uint16_t* spos, int k, bool
           sort_heap(key + lo, idx + lo, hi - lo);
         }
       }
-      break;
+      group_sync<NT>();
+      return 0;
     }
     --depth;
-    if (lane == 0) {
-      move_median_to_first(key, idx, lo, lo + 1, lo + (hi - lo) / 2, hi - 1);
-      sc.gnext = kBig;
+    const int par = level & 1;
+    // ---- median of three, by every lane; the swap into lo stays virtual until after P1 ----
+    const int a = lo + 1, b = lo + (hi - lo) / 2, c = hi - 1;
+    const KeyT ka = key[a], kb = key[b], kc = key[c], klo = key[lo];
+    int ch;
+    if (ka < kb) {
+      if (kb < kc) ch = b; else if (ka < kc) ch = c; else ch = a;
+    } else if (ka < kc) {
+      ch = a;
+    } else if (kb < kc) {
+      ch = c;
+    } else {
+      ch = b;
     }
-    wave_sync();
-    const KeyT p = key[lo];
-    const int J = (hi - lo - 1 + 63) / 64;  // <= 16
+    const KeyT p = (ch == a) ? ka : (ch == b) ? kb : kc;
+    // ---- P1: flags (keys loaded up front) ----
+    const int J = (hi - lo - 1 + NT - 1) / NT;
+    const int wbeg = lo + 1 + wid * J * 64;
+    KeyT kv[JM];
+#pragma unroll
+    for (int j = 0; j < JM; ++j) {
+      const int pos = wbeg + j * 64 + lane;
+      kv[j] = (j < J && pos < hi) ? key[pos] : (KeyT)0;
+    }
     uint32_t gem = 0, lem = 0;
-    int tot_le = 0;
-    for (int j = 0; j < J; ++j) {
-      const int pos = lo + 1 + j * 64 + lane;
-      const bool valid = pos < hi;
-      const KeyT kk = valid ? key[pos] : (KeyT)0;
-      const bool ge = valid && !(kk < p);
-      const bool le = valid && !(p < kk);
-      gem |= (uint32_t)ge << j;
-      lem |= (uint32_t)le << j;
-      tot_le += __popcll(__ballot(le));
-    }
-    int run = 0;
-    for (int j = 0; j < J; ++j) {
-      const bool le = (lem >> j) & 1u;
-      const uint64_t bl = __ballot(le);
-      if (le) {
-        const int incl = run + __popcll(bl & lanemask_le(lane));
-        spos[tot_le - incl + 1] = (uint16_t)(lo + 1 + j * 64 + lane);
+    int cge = 0, cle = 0;
+#pragma unroll
+    for (int j = 0; j < JM; ++j) {
+      if (j < J) {
+        const int pos = wbeg + j * 64 + lane;
+        const bool valid = pos < hi;
+        const KeyT kk = (pos == ch) ? klo : kv[j];
+        const bool ge = valid && !(kk < p);
+        const bool le = valid && !(p < kk);
+        gem |= (uint32_t)ge << j;
+        lem |= (uint32_t)le << j;
+        cge += __popcll(__ballot(ge));
+        cle += __popcll(__ballot(le));
       }
-      run += __popcll(bl);
     }
-    if (lane == 0) spos[tot_le + 1] = (uint16_t)lo;
-    wave_sync();
-    run = 0;
-    msw = 0;
-    for (int j = 0; j < J; ++j) {
-      const bool ge = (gem >> j) & 1u;
-      const uint64_t bg = __ballot(ge);
-      const int t = run + __popcll(bg & lanemask_lt(lane)) + 1;
-      const bool pair = ge && t <= tot_le + 1 && (int)spos[t] > lo + 1 + j * 64 + lane;
-      msw += __popcll(__ballot(pair));
-      run += __popcll(bg);
-    }
-    run = 0;
-    for (int j = 0; j < J; ++j) {
-      const bool ge = (gem >> j) & 1u;
-      const uint64_t bg = __ballot(ge);
-      if (ge) {
-        const int t = run + __popcll(bg & lanemask_lt(lane)) + 1;
-        const int pos = lo + 1 + j * 64 + lane;
-        if (t <= msw)
-          kv_swap(key, idx, pos, (int)spos[t]);
-        else if (t == msw + 1)
-          sc.gnext = pos;
+    int ge_before = 0, le_before = 0, tot_le = cle;
+    if constexpr (NW > 1) {
+      if (lane == 0) {
+        sc.wa[wid] = cge;
+        sc.wb[wid] = cle;
       }
-      run += __popcll(bg);
+      __syncthreads();  // B_a
+      tot_le = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const int x = sc.wa[w], y = sc.wb[w];
+        ge_before += (w < wid) ? x : 0;
+        le_before += (w < wid) ? y : 0;
+        tot_le += y;
+      }
     }
-    wave_sync();
-    gnext = sc.gnext;
+    // ---- P2: s rank table, swap count m, g_{m+1} (stores only) ----
+    if (tid == 0) {
+      kv_swap(key, idx, lo, ch);  // std::__move_median_to_first, made physical
+      sc.m[par ^ 1] = 0;
+      sc.gnext[par ^ 1] = kBig;
+    }
+    int rge = ge_before, rle = le_before, nsw = 0, ff = kBig;
+#pragma unroll
+    for (int j = 0; j < JM; ++j) {
+      if (j < J) {
+        const bool ge = (gem >> j) & 1u, le = (lem >> j) & 1u;
+        const uint64_t bg = __ballot(ge), bl = __ballot(le);
+        const int A = rge + __popcll(bg & lt);
+        const int lin = rle + __popcll(bl & le_m);
+        if (le) spos[tot_le - lin + 1] = (uint16_t)(wbeg + j * 64 + lane);
+        const bool cond = ge && (A + lin < tot_le);
+        nsw += __popcll(__ballot(cond));
+        const uint64_t bf = __ballot(ge && !cond);
+        if (bf && ff == kBig) ff = wbeg + j * 64 + (__ffsll((unsigned long long)bf) - 1);
+        rge += __popcll(bg);
+        rle += __popcll(bl);
+      }
+    }
+    int msw, gnext;
+    if constexpr (NW > 1) {
+      if (lane == 0) {
+        if (nsw) atomicAdd(&sc.m[par], nsw);
+        if (ff != kBig) atomicMin(&sc.gnext[par], ff);
+      }
+      __syncthreads();  // B_b
+      msw = sc.m[par];
+      gnext = sc.gnext[par];
+    } else {
+      wave_sync();
+      msw = nsw;
+      gnext = ff;
+    }
+    // ---- P4: the m swaps (disjoint pairs), 8 positions per batch: spos loads, then key/idx
+    //      loads, then stores ----
+    if (ge_before < msw) {
+      constexpr int JB = 8;
+      rge = ge_before;
+#pragma unroll
+      for (int j0 = 0; j0 < JM; j0 += JB) {
+        int sp[JB];
+        uint32_t act = 0;
+#pragma unroll
+        for (int q = 0; q < JB; ++q) {
+          const int j = j0 + q;
+          sp[q] = 0;
+          if (j < J) {
+            const bool ge = (gem >> j) & 1u;
+            const uint64_t bg = __ballot(ge);
+            const int t = rge + __popcll(bg & lt) + 1;
+            const bool doit = ge && t <= msw;
+            act |= (uint32_t)doit << q;
+            if (doit) sp[q] = (int)spos[t];
+            rge += __popcll(bg);
+          }
+        }
+        KeyT kg[JB], ks[JB];
+        uint16_t ig[JB], is[JB];
+#pragma unroll
+        for (int q = 0; q < JB; ++q) {
+          if ((act >> q) & 1u) {
+            const int pos = wbeg + (j0 + q) * 64 + lane;
+            kg[q] = key[pos];
+            ks[q] = key[sp[q]];
+            ig[q] = idx[pos];
+            is[q] = idx[sp[q]];
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < JB; ++q) {
+          if ((act >> q) & 1u) {
+            const int pos = wbeg + (j0 + q) * 64 + lane;
+            key[pos] = ks[q];
+            key[sp[q]] = kg[q];
+            idx[pos] = is[q];
+            idx[sp[q]] = ig[q];
+          }
+        }
+      }
+    }
+    group_sync<NT>();  // B_c
+    const int cut = min(gnext, msw > 0 ? (int)spos[msw] : kBig);
+    if (topk) {  // std::__introselect: if (cut <= nth) first = cut; else last = cut;
+      if (cut <= k - 1) lo = cut; else hi = cut;
+    } else {     // std::__introsort_loop: recurse right, loop on the left part
+      if (k <= cut) hi = cut; else lo = cut;
+    }
+    ++level;
   }
-  wave_sync();
 }
 
 template <int DT>
@@ -449,6 +556,10 @@ __global__ void __launch_bounds__(kSelThreads)
       }
     }
   }
+  if (tid == 0) {
+    sc.m[0] = 0;
+    sc.gnext[0] = kBig;
+  }
   __syncthreads();
   KVC_STAMP(1);
 
@@ -456,141 +567,16 @@ __global__ void __launch_bounds__(kSelThreads)
   const bool topk = algo == KVC_ALGO_TOPK;
   const bool partial = topk && (int64_t)k * 64 <= n;  // aten TopKImpl.h: use_partial_sort
   const int thr = topk ? 3 : 16;  // introselect / introsort segment threshold
-  int lo = 0, hi = n, depth = 2 * floor_log2(n);  // chain state, owned by thread 0
-  bool first = true;
-  while (true) {
-    if (tid == 0) {
-      int state = 1;
-      if (partial) {
-        heap_select(key, idx, k, n);  // std::partial_sort's heap select; set = first k
-      } else {
-        if (!first) {  // finish the previous partition: cut = min(g_{m+1}, s_m)
-          const int cut = min(sc.gnext, sc.m > 0 ? (int)spos[sc.m] : kBig);
-          if (topk) {  // std::__introselect: if (cut <= nth) first = cut; else last = cut;
-            if (cut <= k - 1) lo = cut; else hi = cut;
-          } else {     // std::__introsort_loop: right part recursed, loop on the left
-            if (k <= cut) hi = cut; else lo = cut;
-          }
-        }
-        if (lo == k || hi == k) {
-          // a partition boundary sits exactly at k: the first-k set is final
-        } else if (hi - lo <= kWaveSeg) {
-          state = 2;  // short segment: wave 0 finishes the chain without block barriers
-          sc.lo = lo;
-          sc.hi = hi;
-          sc.depth = depth;
-        } else if (depth == 0) {  // depth limit: libstdc++ switches to heap algorithms
-          if (topk) {
-            heap_select(key + lo, idx + lo, k - lo, hi - lo);
-            kv_swap(key, idx, lo, k - 1);
-          } else {
-            make_heap(key + lo, idx + lo, hi - lo);
-            sort_heap(key + lo, idx + lo, hi - lo);
-          }
-        } else {
-          --depth;
-          move_median_to_first(key, idx, lo, lo + 1, lo + (hi - lo) / 2, hi - 1);
-          sc.p = key[lo];
-          sc.lo = lo;
-          sc.hi = hi;
-          sc.m = 0;
-          sc.gnext = kBig;
-          state = 0;
-        }
-      }
-      sc.state = state;
-    }
-    first = false;
-    __syncthreads();
-    if (sc.state) break;
-
-    // ---- one std::__unguarded_partition(lo+1, hi, pivot=lo), computed in parallel ----
-    // g_t: t-th position (ascending) in [lo+1,hi) with !(key < p); s_t: t-th position
-    // (descending) with !(p < key), followed by the pivot slot lo.  libstdc++ swaps g_t<->s_t
-    // for every t with g_t < s_t (a prefix of t) and returns min(g_{m+1}, s_m).
-    const int plo = sc.lo, phi = sc.hi;
-    const KeyT p = sc.p;
-    const int m1 = phi - plo - 1;
-    const int J = (m1 + kSelThreads - 1) / kSelThreads;  // <= 16 positions per lane
-    const int wbeg = plo + 1 + wid * J * 64;
-    uint32_t gem = 0, lem = 0;
-    int cge = 0, cle = 0;
-    for (int j = 0; j < J; ++j) {
-      const int pos = wbeg + j * 64 + lane;
-      const bool valid = pos < phi;
-      const KeyT kk = valid ? key[pos] : (KeyT)0;
-      const bool ge = valid && !(kk < p);
-      const bool le = valid && !(p < kk);
-      gem |= (uint32_t)ge << j;
-      lem |= (uint32_t)le << j;
-      cge += __popcll(__ballot(ge));
-      cle += __popcll(__ballot(le));
-    }
-    if (lane == 0) {
-      sc.wa[wid] = cge;
-      sc.wb[wid] = cle;
-    }
-    __syncthreads();
-    int ge_before = 0, le_before = 0, tot_le = 0;
-    for (int w = 0; w < kSelWaves; ++w) {
-      const int a = sc.wa[w], bb = sc.wb[w];
-      if (w < wid) {
-        ge_before += a;
-        le_before += bb;
-      }
-      tot_le += bb;
-    }
-    {  // s positions by descending rank (1-based); the pivot slot closes the list
-      int run = le_before;
-      for (int j = 0; j < J; ++j) {
-        const bool le = (lem >> j) & 1u;
-        const uint64_t bl = __ballot(le);
-        if (le) {
-          const int incl = run + __popcll(bl & lanemask_le(lane));
-          spos[tot_le - incl + 1] = (uint16_t)(wbeg + j * 64 + lane);
-        }
-        run += __popcll(bl);
-      }
-      if (tid == 0) spos[tot_le + 1] = (uint16_t)plo;
-    }
-    __syncthreads();
-    {  // number of swaps m = #{t : g_t < s_t}
-      int run = ge_before, cnt = 0;
-      for (int j = 0; j < J; ++j) {
-        const bool ge = (gem >> j) & 1u;
-        const uint64_t bg = __ballot(ge);
-        if (ge) {
-          const int t = run + __popcll(bg & lanemask_lt(lane)) + 1;
-          if (t <= tot_le + 1 && (int)spos[t] > wbeg + j * 64 + lane) ++cnt;
-        }
-        run += __popcll(bg);
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-      if (lane == 0 && cnt) atomicAdd(&sc.m, cnt);
-    }
-    __syncthreads();
-    {  // the swaps (all pairs are disjoint) and g_{m+1}
-      const int msw = sc.m;
-      int run = ge_before;
-      for (int j = 0; j < J; ++j) {
-        const bool ge = (gem >> j) & 1u;
-        const uint64_t bg = __ballot(ge);
-        if (ge) {
-          const int t = run + __popcll(bg & lanemask_lt(lane)) + 1;
-          const int pos = wbeg + j * 64 + lane;
-          if (t <= msw)
-            kv_swap(key, idx, pos, (int)spos[t]);
-          else if (t == msw + 1)
-            sc.gnext = pos;
-        }
-        run += __popcll(bg);
-      }
-    }
-    __syncthreads();
+  if (partial) {
+    if (tid == 0) heap_select(key, idx, k, n);  // std::partial_sort's heap select
+  } else {
+    int lo = 0, hi = n, depth = 2 * floor_log2(n), level = 0;
+    const int st = run_chain<KeyT, kSelThreads>(key, idx, spos, sc, k, topk, thr, lo, hi, depth,
+                                                level);
+    KVC_STAMP(2);
+    if (st == 1 && wid == 0)
+      run_chain<KeyT, 64>(key, idx, spos, sc, k, topk, thr, lo, hi, depth, level);
   }
-  KVC_STAMP(2);
-  if (sc.state == 2 && wid == 0) wave_chain(key, idx, spos, k, topk, thr, sc.lo, sc.hi, sc.depth, sc);
   __syncthreads();
   KVC_STAMP(3);
 

@@ -6,7 +6,6 @@ arithmetic) and, for every layer that the reference would gather/concatenate, re
 batched engine launch per (device, dtype, batch, heads, head_dim) group -- score, select and
 gather kernels over every layer at once -- and writes the new (K, V) tensors back into the list.
 """
-import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -102,25 +101,6 @@ def execute(jobs: List[Segments], out_list: list, order: int, algo: int):
         _run_group(device, dtype, B, H, D, js, out_list, order, algo)
 
 
-def _pipeline_chunks(n_layers, external):
-    """Layer chunks for the score/select pipeline (KVC_PIPELINE_CHUNKS overrides; 1 = serial)."""
-    env = os.environ.get("KVC_PIPELINE_CHUNKS")
-    c = int(env) if env else (4 if n_layers >= 8 else 1)
-    if external or n_layers < 2:
-        return 1
-    return max(1, min(c, n_layers))
-
-
-_side_streams = {}
-
-
-def _side_stream(device):
-    s = _side_streams.get(device)
-    if s is None:
-        s = _side_streams[device] = torch.cuda.Stream(device=device)
-    return s
-
-
 def _upload(params, table, device, js, B, H):
     """Plan one table, allocate its workspace and enqueue the descriptor upload (current stream)."""
     rc, info = N.plan(params, table)
@@ -191,33 +171,12 @@ def _run_group(device, dtype, B, H, D, js, out_list, order, algo):
                         algo=algo, phases=N.PHASE_GATHER if external else N.PHASE_ALL,
                         external_index=1 if external else 0)
 
-    C = _pipeline_chunks(n, external)
-    bounds = [n * c // C for c in range(C + 1)]
+    # One launch (score, select, gather kernels) for every layer of the group.  (Pipelining
+    # layer chunks over two streams -- score of chunk c+1 beside select of chunk c -- was
+    # measured slower at 2/4/8 chunks: profiles/r01_pipeline_sweep.json.)
     with torch.cuda.device(device):
-        main = torch.cuda.current_stream(device)
-        chunks = []
-        for c in range(C):
-            sub = table[bounds[c]:bounds[c + 1]].copy()
-            p = params()
-            ws, info = _upload(p, sub, device, js[bounds[c]:bounds[c + 1]], B, H)
-            chunks.append((p, sub, ws, info))
-        if C == 1:
-            p, sub, ws, info = chunks[0]
-            _launch(p, sub, ws, info, main, p.phases)
-        else:
-            # score chunk c+1 on a side stream while chunk c selects/gathers on the caller's
-            # stream; the caller's stream waits for every score event, so all side-stream work
-            # is complete (stream-ordered) before anything later on the caller's stream runs.
-            side = _side_stream(device)
-            side.wait_stream(main)
-            events = []
-            for p, sub, ws, info in chunks:
-                _launch(p, sub, ws, info, side, N.PHASE_SCORE)
-                ev = torch.cuda.Event()
-                ev.record(side)
-                events.append(ev)
-            for (p, sub, ws, info), ev in zip(chunks, events):
-                main.wait_event(ev)
-                _launch(p, sub, ws, info, main, N.PHASE_SELECT | N.PHASE_GATHER)
+        p = params()
+        ws, info = _upload(p, table, device, js, B, H)
+        _launch(p, table, ws, info, torch.cuda.current_stream(device), p.phases)
     for j, (ko, vo) in zip(js, outs):
         out_list[j.layer_idx] = (ko, vo)
