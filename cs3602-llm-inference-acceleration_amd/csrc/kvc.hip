@@ -79,7 +79,7 @@ __device__ __forceinline__ typename DTypeTraits<DT>::key_t key_of(float f, bool 
 #ifdef KVC_STAMPS
 #define KVC_STAMP(i)                                                             \
   do {                                                                           \
-    if (stamps && threadIdx.x == 0) stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+    if (stamps && threadIdx.x == 0) stamps[blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
 #define KVC_STAMP(i) \
@@ -297,9 +297,17 @@ __device__ __forceinline__ void group_sync() {
 // (lane + 64*j within a wave's stripe) so ge/le flags are wave ballots; every j-loop is fully
 // unrolled and loads are issued before dependent stores, keeping LDS latency off the chain.
 // Returns 0 when the first-k set is final, 1 when the block hands a short segment to one wave.
+#ifdef KVC_STAMPS
+#define KVC_TICK(v) (v) = __builtin_amdgcn_s_memtime()
+#else
+#define KVC_TICK(v) (void)0
+#endif
+
 template <typename KeyT, int NT>
 __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, SelScalars<KeyT>& sc, int k,
-                         bool topk, int thr, int& lo, int& hi, int& depth, int& level) {
+                         bool topk, int thr, int& lo, int& hi, int& depth, int& level,
+                         uint64_t* acc = nullptr) {
+  uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
   constexpr int NW = NT / 64;
   constexpr int JM = 16;  // positions per lane: n <= 16384 at NT = 1024, m <= 1024 at NT = 64
   const int lane = threadIdx.x & 63;
@@ -328,6 +336,7 @@ __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, SelScalars<Ke
       return 0;
     }
     --depth;
+    KVC_TICK(t0);
     const int par = level & 1;
     // ---- median of three, by every lane; the swap into lo stays virtual until after P1 ----
     const int a = lo + 1, b = lo + (hi - lo) / 2, c = hi - 1;
@@ -384,6 +393,7 @@ __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, SelScalars<Ke
         tot_le += y;
       }
     }
+    KVC_TICK(t1);
     // ---- P2: s rank table, swap count m, g_{m+1} (stores only) ----
     if (tid == 0) {
       kv_swap(key, idx, lo, ch);  // std::__move_median_to_first, made physical
@@ -421,6 +431,7 @@ __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, SelScalars<Ke
       msw = nsw;
       gnext = ff;
     }
+    KVC_TICK(t2);
     // ---- P4: the m swaps (disjoint pairs), 8 positions per batch: spos loads, then key/idx
     //      loads, then stores ----
     if (ge_before < msw) {
@@ -469,6 +480,16 @@ __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, SelScalars<Ke
       }
     }
     group_sync<NT>();  // B_c
+    KVC_TICK(t3);
+#ifdef KVC_STAMPS
+    if (acc && tid == 0) {
+      acc[0] += t1 - t0;
+      acc[1] += t2 - t1;
+      acc[2] += t3 - t2;
+      acc[3] += 1;
+      acc[4] += (uint64_t)msw;
+    }
+#endif
     const int cut = min(gnext, msw > 0 ? (int)spos[msw] : kBig);
     if (topk) {  // std::__introselect: if (cut <= nth) first = cut; else last = cut;
       if (cut <= k - 1) lo = cut; else hi = cut;
@@ -571,11 +592,21 @@ __global__ void __launch_bounds__(kSelThreads)
     if (tid == 0) heap_select(key, idx, k, n);  // std::partial_sort's heap select
   } else {
     int lo = 0, hi = n, depth = 2 * floor_log2(n), level = 0;
+    uint64_t* accb = nullptr;
+    uint64_t* accw = nullptr;
+#ifdef KVC_STAMPS
+    if (stamps) {
+      accb = stamps + blockIdx.x * 16 + 5;
+      accw = stamps + blockIdx.x * 16 + 10;
+      if (tid == 0)
+        for (int q = 0; q < 10; ++q) accb[q] = 0;
+    }
+#endif
     const int st = run_chain<KeyT, kSelThreads>(key, idx, spos, sc, k, topk, thr, lo, hi, depth,
-                                                level);
+                                                level, accb);
     KVC_STAMP(2);
     if (st == 1 && wid == 0)
-      run_chain<KeyT, 64>(key, idx, spos, sc, k, topk, thr, lo, hi, depth, level);
+      run_chain<KeyT, 64>(key, idx, spos, sc, k, topk, thr, lo, hi, depth, level, accw);
   }
   __syncthreads();
   KVC_STAMP(3);
@@ -802,7 +833,7 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
     info->index_offset = off;
     off = round_up(off + (size_t)rows * info->index_row_stride * 4, 256);
 #ifdef KVC_STAMPS
-    off += (size_t)rows * 64;  // diagnostic stamp slots (8 x u64 per select row)
+    off += (size_t)rows * 128;  // diagnostic stamp slots (16 x u64 per select row)
 #endif
     info->workspace_bytes = off;
   }
@@ -906,7 +937,7 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
   bool any_sel = false;
   for (int l = 0; l < nl; ++l) any_sel |= layers[l].n_select > 0;
 #ifdef KVC_STAMPS
-  uint64_t* stamps = reinterpret_cast<uint64_t*>(w + info.workspace_bytes - info.rows * 64);
+  uint64_t* stamps = reinterpret_cast<uint64_t*>(w + info.workspace_bytes - info.rows * 128);
 #else
   uint64_t* stamps = nullptr;
 #endif

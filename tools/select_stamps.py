@@ -40,7 +40,14 @@ for rep in range(3):
     assert rc == 0
     torch.cuda.synchronize()
 rows = int(info.rows)
-st = ws[-rows * 64:].view(torch.int64).view(rows, 8).cpu().numpy()[:, :5].astype(np.float64)
+allst = ws[-rows * 128:].view(torch.int64).view(rows, 16).cpu().numpy().astype(np.float64)
+st = allst[:, :5]
+for nm, off in (("block", 5), ("wave", 10)):
+    acc = allst[:, off:off + 5]
+    res[nm + "_levels_median"] = float(np.median(acc[:, 3]))
+    res[nm + "_swaps_per_level_median"] = float(np.median(acc[:, 4] / np.maximum(acc[:, 3], 1)))
+    for q, pn in enumerate(("median+P1", "P2", "P4")):
+        res[f"{nm}_{pn}_cycles_per_level"] = float(np.median(acc[:, q] / np.maximum(acc[:, 3], 1)))
 d = np.diff(st, axis=1)
 names = ["key_load", "block_chain", "wave_chain", "emit"]
 res["median_cycles"] = {n: float(np.median(d[:, i])) for i, n in enumerate(names)}
