@@ -32,7 +32,7 @@ constexpr int kScoreWaves = kScoreThreads / 64;
 constexpr int kSelThreads = 1024;
 constexpr int kSelWaves = kSelThreads / 64;
 constexpr int kZoneMax = 16384;  // longest zone whose keys fit the select kernel's LDS
-constexpr int kWaveSeg = 1024;   // segments this short are finished by one wave (no block barriers)
+constexpr int kWaveSeg = 1024;   // default: segments this short are finished by one wave
 constexpr int kGatherThreads = 256;
 constexpr int kGatherTokens = 64;  // output tokens per gather block
 constexpr int kBig = 0x7FFFFFFF;
@@ -306,7 +306,7 @@ __device__ __forceinline__ void group_sync() {
 template <typename KeyT, int NT>
 __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, SelScalars<KeyT>& sc, int k,
                          bool topk, int thr, int& lo, int& hi, int& depth, int& level,
-                         uint64_t* acc = nullptr) {
+                         int wave_seg, uint64_t* acc = nullptr) {
   uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
   constexpr int NW = NT / 64;
   constexpr int JM = 16;  // positions per lane: n <= 16384 at NT = 1024, m <= 1024 at NT = 64
@@ -321,7 +321,7 @@ __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, SelScalars<Ke
       group_sync<NT>();
       return 0;
     }
-    if (NT > 64 && hi - lo <= kWaveSeg) return 1;
+    if (NT > 64 && hi - lo <= wave_seg) return 1;
     if (depth == 0) {  // depth limit: libstdc++ switches to heap algorithms
       if (tid == 0) {
         if (topk) {
@@ -504,7 +504,8 @@ template <int DT>
 __global__ void __launch_bounds__(kSelThreads)
     select_kernel(const kvc_layer_t* __restrict__ L, int BH, int order, int algo,
                   const char* __restrict__ norms, int64_t norm_stride,
-                  int32_t* __restrict__ out_idx, int64_t idx_stride, uint64_t* stamps) {
+                  int32_t* __restrict__ out_idx, int64_t idx_stride, int wave_seg,
+                  uint64_t* stamps) {
   typedef typename DTypeTraits<DT>::key_t KeyT;
   constexpr int ESZ = DTypeTraits<DT>::esz;
   // LDS: key[kZoneMax] | idx[kZoneMax] (u16) | spos[kZoneMax + 8] (u16) | scalars
@@ -603,10 +604,10 @@ __global__ void __launch_bounds__(kSelThreads)
     }
 #endif
     const int st = run_chain<KeyT, kSelThreads>(key, idx, spos, sc, k, topk, thr, lo, hi, depth,
-                                                level, accb);
+                                                level, wave_seg, accb);
     KVC_STAMP(2);
     if (st == 1 && wid == 0)
-      run_chain<KeyT, 64>(key, idx, spos, sc, k, topk, thr, lo, hi, depth, level, accw);
+      run_chain<KeyT, 64>(key, idx, spos, sc, k, topk, thr, lo, hi, depth, level, wave_seg, accw);
   }
   __syncthreads();
   KVC_STAMP(3);
@@ -936,6 +937,12 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
   int32_t* idx = reinterpret_cast<int32_t*>(w + info.index_offset);
   bool any_sel = false;
   for (int l = 0; l < nl; ++l) any_sel |= layers[l].n_select > 0;
+  // wave hand-off threshold (<= 1024: the wave chain covers 64 lanes x 16 positions);
+  // KVC_WAVE_SEG overrides it for tuning sweeps
+  int wave_seg = kWaveSeg;
+  if (const char* e = getenv("KVC_WAVE_SEG")) wave_seg = atoi(e);
+  if (wave_seg < 16) wave_seg = 16;
+  if (wave_seg > 1024) wave_seg = 1024;
 #ifdef KVC_STAMPS
   uint64_t* stamps = reinterpret_cast<uint64_t*>(w + info.workspace_bytes - info.rows * 128);
 #else
@@ -954,10 +961,10 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
     const dim3 grid((unsigned)info.rows), block(kSelThreads);
     if (p->dtype == KVC_BF16)
       hipLaunchKernelGGL(select_kernel<KVC_BF16>, grid, block, 0, s, layers_dev, BH, p->order,
-                         p->algo, norms, info.norm_row_stride, idx, info.index_row_stride, stamps);
+                         p->algo, norms, info.norm_row_stride, idx, info.index_row_stride, wave_seg, stamps);
     else
       hipLaunchKernelGGL(select_kernel<KVC_F32>, grid, block, 0, s, layers_dev, BH, p->order,
-                         p->algo, norms, info.norm_row_stride, idx, info.index_row_stride, stamps);
+                         p->algo, norms, info.norm_row_stride, idx, info.index_row_stride, wave_seg, stamps);
   }
   if ((p->phases & KVC_PHASE_GATHER) && info.gather_units > 0) {
     int64_t max_out = 0;

@@ -25,6 +25,9 @@ if [ "$MODE" = "micro" ]; then
   cat gpurun_out/micro.json
 fi
 if [ "$MODE" = "stamps" ]; then
-  timeout -k 10 300 python tools/select_stamps.py > gpurun_out/stamps.json 2> gpurun_out/stamps.err || exit $?
+  : > gpurun_out/stamps.json
+  for ws in ${2:-1024}; do
+    KVC_WAVE_SEG=$ws timeout -k 10 300 python tools/select_stamps.py >> gpurun_out/stamps.json 2>> gpurun_out/stamps.err || exit $?
+  done
   cat gpurun_out/stamps.json
 fi

@@ -33,7 +33,7 @@ p = N.Params(dtype=N.KVC_BF16, batch=1, heads=H, head_dim=D, order=0, algo=0,
 rc, info = N.plan(p, table)
 assert rc == 0
 ws = torch.zeros(int(info.workspace_bytes), dtype=torch.uint8, device=dev)
-res = {}
+res = {"wave_seg": os.environ.get("KVC_WAVE_SEG", "default")}
 for rep in range(3):
     rc = N.launch(p, table, 0, ws.data_ptr(), int(info.workspace_bytes),
                   torch.cuda.current_stream().cuda_stream)
