@@ -303,17 +303,177 @@ __device__ __forceinline__ void group_sync() {
 #define KVC_TICK(v) (void)0
 #endif
 
-template <typename KeyT, int NT>
-__device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, SelScalars<KeyT>& sc, int k,
-                         bool topk, int thr, int& lo, int& hi, int& depth, int& level,
-                         int wave_seg, uint64_t* acc = nullptr) {
-  uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+// One partition level over [lo, hi) with at most JM positions per lane (compile-time, so the
+// passes are branch-free straight-line code).  Returns cut.  See run_chain for the algorithm.
+template <typename KeyT, int NT, int JM>
+__device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_t* spos,
+                                               SelScalars<KeyT>& sc, int lo, int hi, int par,
+                                               uint64_t* acc) {
   constexpr int NW = NT / 64;
-  constexpr int JM = 16;  // positions per lane: n <= 16384 at NT = 1024, m <= 1024 at NT = 64
   const int lane = threadIdx.x & 63;
   const int wid = (NT == 64) ? 0 : (int)(threadIdx.x >> 6);
   const int tid = wid * 64 + lane;
   const uint64_t lt = lanemask_lt(lane), le_m = lanemask_le(lane);
+  uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+  KVC_TICK(t0);
+  const int J = (hi - lo - 1 + NT - 1) / NT;  // <= JM
+  const int wbeg = lo + 1 + wid * J * 64;
+  // ---- loads first: median candidates, the pivot slot and this lane's keys ----
+  const int a = lo + 1, b = lo + (hi - lo) / 2, c = hi - 1;
+  const KeyT ka = key[a], kb = key[b], kc = key[c], klo = key[lo];
+  // std::__move_median_to_first, evaluated by every lane; the swap into lo stays virtual
+  int ch;
+  if (ka < kb) {
+    if (kb < kc) ch = b; else if (ka < kc) ch = c; else ch = a;
+  } else if (ka < kc) {
+    ch = a;
+  } else if (kb < kc) {
+    ch = c;
+  } else {
+    ch = b;
+  }
+  const KeyT p = (ch == a) ? ka : (ch == b) ? kb : kc;
+  // ---- P1: ge/le flags ----
+  uint32_t gem = 0, lem = 0;
+  int cge = 0, cle = 0;
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+    const int pos = wbeg + j * 64 + lane;
+    const bool valid = (j < J) && (pos < hi);
+    const KeyT kk = (pos == ch) ? klo : key[min(pos, hi - 1)];
+    const bool ge = valid && !(kk < p);
+    const bool le = valid && !(p < kk);
+    gem |= (uint32_t)ge << j;
+    lem |= (uint32_t)le << j;
+    cge += __popcll(__ballot(ge));
+    cle += __popcll(__ballot(le));
+  }
+  int ge_before = 0, le_before = 0, tot_le = cle;
+  if constexpr (NW > 1) {
+    if (lane == 0) {
+      sc.wa[wid] = cge;
+      sc.wb[wid] = cle;
+    }
+    __syncthreads();  // B_a
+    tot_le = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const int x = sc.wa[w], y = sc.wb[w];
+      ge_before += (w < wid) ? x : 0;
+      le_before += (w < wid) ? y : 0;
+      tot_le += y;
+    }
+  }
+  KVC_TICK(t1);
+  // ---- P2: s rank table, swap count m, g_{m+1} (stores only) ----
+  if (tid == 0) {
+    kv_swap(key, idx, lo, ch);  // the median move, made physical
+    sc.m[par ^ 1] = 0;
+    sc.gnext[par ^ 1] = kBig;
+  }
+  int rge = ge_before, rle = le_before, nsw = 0, ff = kBig;
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+    const bool ge = (gem >> j) & 1u, le = (lem >> j) & 1u;
+    const uint64_t bg = __ballot(ge), bl = __ballot(le);
+    const int A = rge + __popcll(bg & lt);
+    const int lin = rle + __popcll(bl & le_m);
+    if (le) spos[tot_le - lin + 1] = (uint16_t)(wbeg + j * 64 + lane);
+    const bool cond = ge && (A + lin < tot_le);
+    nsw += __popcll(__ballot(cond));
+    const uint64_t bf = __ballot(ge && !cond);
+    if (bf && ff == kBig) ff = wbeg + j * 64 + (__ffsll((unsigned long long)bf) - 1);
+    rge += __popcll(bg);
+    rle += __popcll(bl);
+  }
+  int msw, gnext;
+  if constexpr (NW > 1) {
+    if (lane == 0) {
+      if (nsw) atomicAdd(&sc.m[par], nsw);
+      if (ff != kBig) atomicMin(&sc.gnext[par], ff);
+    }
+    __syncthreads();  // B_b
+    msw = sc.m[par];
+    gnext = sc.gnext[par];
+  } else {
+    wave_sync();
+    msw = nsw;
+    gnext = ff;
+  }
+  KVC_TICK(t2);
+  // ---- P4: the m swaps (disjoint pairs) in batches: spos loads, key/idx loads, stores ----
+  if (ge_before < msw) {
+    constexpr int JB = JM < 4 ? JM : 4;
+    rge = ge_before;
+#pragma unroll
+    for (int j0 = 0; j0 < JM; j0 += JB) {
+      int sp[JB];
+      uint32_t act = 0;
+#pragma unroll
+      for (int q = 0; q < JB; ++q) {
+        const bool ge = (gem >> (j0 + q)) & 1u;
+        const uint64_t bg = __ballot(ge);
+        const int t = rge + __popcll(bg & lt) + 1;
+        const bool doit = ge && t <= msw;
+        act |= (uint32_t)doit << q;
+        sp[q] = spos[doit ? t : 0];
+        rge += __popcll(bg);
+      }
+      KeyT kg[JB], ks[JB];
+      uint16_t ig[JB], is[JB];
+#pragma unroll
+      for (int q = 0; q < JB; ++q) {
+        const int pos = min(wbeg + (j0 + q) * 64 + lane, hi - 1);
+        kg[q] = key[pos];
+        ks[q] = key[sp[q]];
+        ig[q] = idx[pos];
+        is[q] = idx[sp[q]];
+      }
+#pragma unroll
+      for (int q = 0; q < JB; ++q) {
+        if ((act >> q) & 1u) {
+          const int pos = wbeg + (j0 + q) * 64 + lane;
+          key[pos] = ks[q];
+          key[sp[q]] = kg[q];
+          idx[pos] = is[q];
+          idx[sp[q]] = ig[q];
+        }
+      }
+    }
+  }
+  group_sync<NT>();  // B_c
+  KVC_TICK(t3);
+#ifdef KVC_STAMPS
+  if (acc && tid == 0) {
+    acc[0] += t1 - t0;
+    acc[1] += t2 - t1;
+    acc[2] += t3 - t2;
+    acc[3] += 1;
+    acc[4] += (uint64_t)msw;
+  }
+#endif
+  return min(gnext, msw > 0 ? (int)spos[msw] : kBig);
+}
+
+// The partition chain of libstdc++ introsort (topk = false) / introselect (topk = true),
+// following only the segment [lo, hi) that straddles position k, run by NT cooperating lanes
+// (the whole 1024-thread block, or one wave once the segment is short).  One level is
+// std::__move_median_to_first + std::__unguarded_partition(lo+1, hi, pivot=lo) computed in
+// parallel:
+//   g_t = t-th position (ascending) in [lo+1,hi) with !(key < p)            ("ge")
+//   s_t = t-th position (descending) with !(p < key), then the pivot slot lo ("le")
+// libstdc++ swaps g_t <-> s_t for every t with g_t < s_t -- a prefix t <= m -- and returns
+// cut = min(g_{m+1}, s_m).  With A(x) = #ge before x and Lin(x) = #le in [lo+1, x]:
+//   g_t < s_t  <=>  A(g_t) + Lin(g_t) < tot_le
+// so m is counted in the same pass that scatters the s rank -> position table (spos).
+// Positions are laid out j-major (lane + 64*j within a wave's stripe) so flags are wave ballots;
+// each level runs a body specialised on its positions-per-lane bound (1..16).
+// Returns 0 when the first-k set is final, 1 when the block hands a short segment to one wave.
+template <typename KeyT, int NT>
+__device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, SelScalars<KeyT>& sc, int k,
+                         bool topk, int thr, int& lo, int& hi, int& depth, int& level,
+                         int wave_seg, uint64_t* acc = nullptr) {
+  const int tid = (NT == 64) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   while (true) {
     if (lo == k || hi == k) return 0;  // a partition boundary sits at k: the set is final
     if (hi - lo <= thr) {              // final (stable) insertion sort of the segment
@@ -336,161 +496,19 @@ __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, SelScalars<Ke
       return 0;
     }
     --depth;
-    KVC_TICK(t0);
     const int par = level & 1;
-    // ---- median of three, by every lane; the swap into lo stays virtual until after P1 ----
-    const int a = lo + 1, b = lo + (hi - lo) / 2, c = hi - 1;
-    const KeyT ka = key[a], kb = key[b], kc = key[c], klo = key[lo];
-    int ch;
-    if (ka < kb) {
-      if (kb < kc) ch = b; else if (ka < kc) ch = c; else ch = a;
-    } else if (ka < kc) {
-      ch = a;
-    } else if (kb < kc) {
-      ch = c;
-    } else {
-      ch = b;
-    }
-    const KeyT p = (ch == a) ? ka : (ch == b) ? kb : kc;
-    // ---- P1: flags (keys loaded up front) ----
     const int J = (hi - lo - 1 + NT - 1) / NT;
-    const int wbeg = lo + 1 + wid * J * 64;
-    KeyT kv[JM];
-#pragma unroll
-    for (int j = 0; j < JM; ++j) {
-      const int pos = wbeg + j * 64 + lane;
-      kv[j] = (j < J && pos < hi) ? key[pos] : (KeyT)0;
-    }
-    uint32_t gem = 0, lem = 0;
-    int cge = 0, cle = 0;
-#pragma unroll
-    for (int j = 0; j < JM; ++j) {
-      if (j < J) {
-        const int pos = wbeg + j * 64 + lane;
-        const bool valid = pos < hi;
-        const KeyT kk = (pos == ch) ? klo : kv[j];
-        const bool ge = valid && !(kk < p);
-        const bool le = valid && !(p < kk);
-        gem |= (uint32_t)ge << j;
-        lem |= (uint32_t)le << j;
-        cge += __popcll(__ballot(ge));
-        cle += __popcll(__ballot(le));
-      }
-    }
-    int ge_before = 0, le_before = 0, tot_le = cle;
-    if constexpr (NW > 1) {
-      if (lane == 0) {
-        sc.wa[wid] = cge;
-        sc.wb[wid] = cle;
-      }
-      __syncthreads();  // B_a
-      tot_le = 0;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        const int x = sc.wa[w], y = sc.wb[w];
-        ge_before += (w < wid) ? x : 0;
-        le_before += (w < wid) ? y : 0;
-        tot_le += y;
-      }
-    }
-    KVC_TICK(t1);
-    // ---- P2: s rank table, swap count m, g_{m+1} (stores only) ----
-    if (tid == 0) {
-      kv_swap(key, idx, lo, ch);  // std::__move_median_to_first, made physical
-      sc.m[par ^ 1] = 0;
-      sc.gnext[par ^ 1] = kBig;
-    }
-    int rge = ge_before, rle = le_before, nsw = 0, ff = kBig;
-#pragma unroll
-    for (int j = 0; j < JM; ++j) {
-      if (j < J) {
-        const bool ge = (gem >> j) & 1u, le = (lem >> j) & 1u;
-        const uint64_t bg = __ballot(ge), bl = __ballot(le);
-        const int A = rge + __popcll(bg & lt);
-        const int lin = rle + __popcll(bl & le_m);
-        if (le) spos[tot_le - lin + 1] = (uint16_t)(wbeg + j * 64 + lane);
-        const bool cond = ge && (A + lin < tot_le);
-        nsw += __popcll(__ballot(cond));
-        const uint64_t bf = __ballot(ge && !cond);
-        if (bf && ff == kBig) ff = wbeg + j * 64 + (__ffsll((unsigned long long)bf) - 1);
-        rge += __popcll(bg);
-        rle += __popcll(bl);
-      }
-    }
-    int msw, gnext;
-    if constexpr (NW > 1) {
-      if (lane == 0) {
-        if (nsw) atomicAdd(&sc.m[par], nsw);
-        if (ff != kBig) atomicMin(&sc.gnext[par], ff);
-      }
-      __syncthreads();  // B_b
-      msw = sc.m[par];
-      gnext = sc.gnext[par];
-    } else {
-      wave_sync();
-      msw = nsw;
-      gnext = ff;
-    }
-    KVC_TICK(t2);
-    // ---- P4: the m swaps (disjoint pairs), 8 positions per batch: spos loads, then key/idx
-    //      loads, then stores ----
-    if (ge_before < msw) {
-      constexpr int JB = 8;
-      rge = ge_before;
-#pragma unroll
-      for (int j0 = 0; j0 < JM; j0 += JB) {
-        int sp[JB];
-        uint32_t act = 0;
-#pragma unroll
-        for (int q = 0; q < JB; ++q) {
-          const int j = j0 + q;
-          sp[q] = 0;
-          if (j < J) {
-            const bool ge = (gem >> j) & 1u;
-            const uint64_t bg = __ballot(ge);
-            const int t = rge + __popcll(bg & lt) + 1;
-            const bool doit = ge && t <= msw;
-            act |= (uint32_t)doit << q;
-            if (doit) sp[q] = (int)spos[t];
-            rge += __popcll(bg);
-          }
-        }
-        KeyT kg[JB], ks[JB];
-        uint16_t ig[JB], is[JB];
-#pragma unroll
-        for (int q = 0; q < JB; ++q) {
-          if ((act >> q) & 1u) {
-            const int pos = wbeg + (j0 + q) * 64 + lane;
-            kg[q] = key[pos];
-            ks[q] = key[sp[q]];
-            ig[q] = idx[pos];
-            is[q] = idx[sp[q]];
-          }
-        }
-#pragma unroll
-        for (int q = 0; q < JB; ++q) {
-          if ((act >> q) & 1u) {
-            const int pos = wbeg + (j0 + q) * 64 + lane;
-            key[pos] = ks[q];
-            key[sp[q]] = kg[q];
-            idx[pos] = is[q];
-            idx[sp[q]] = ig[q];
-          }
-        }
-      }
-    }
-    group_sync<NT>();  // B_c
-    KVC_TICK(t3);
-#ifdef KVC_STAMPS
-    if (acc && tid == 0) {
-      acc[0] += t1 - t0;
-      acc[1] += t2 - t1;
-      acc[2] += t3 - t2;
-      acc[3] += 1;
-      acc[4] += (uint64_t)msw;
-    }
-#endif
-    const int cut = min(gnext, msw > 0 ? (int)spos[msw] : kBig);
+    int cut;
+    if (J <= 1)
+      cut = partition_level<KeyT, NT, 1>(key, idx, spos, sc, lo, hi, par, acc);
+    else if (J <= 2)
+      cut = partition_level<KeyT, NT, 2>(key, idx, spos, sc, lo, hi, par, acc);
+    else if (J <= 4)
+      cut = partition_level<KeyT, NT, 4>(key, idx, spos, sc, lo, hi, par, acc);
+    else if (J <= 8)
+      cut = partition_level<KeyT, NT, 8>(key, idx, spos, sc, lo, hi, par, acc);
+    else
+      cut = partition_level<KeyT, NT, 16>(key, idx, spos, sc, lo, hi, par, acc);
     if (topk) {  // std::__introselect: if (cut <= nth) first = cut; else last = cut;
       if (cut <= k - 1) lo = cut; else hi = cut;
     } else {     // std::__introsort_loop: recurse right, loop on the left part
