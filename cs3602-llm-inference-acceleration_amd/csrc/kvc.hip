@@ -32,7 +32,7 @@ constexpr int kScoreWaves = kScoreThreads / 64;
 constexpr int kSelThreads = 1024;
 constexpr int kSelWaves = kSelThreads / 64;
 constexpr int kZoneMax = 16384;  // longest zone whose keys fit the select kernel's LDS
-constexpr int kWaveSeg = 1024;   // default: segments this short are finished by one wave
+constexpr int kWaveSeg = 128;    // default: segments this short are finished by one wave
 constexpr int kGatherThreads = 256;
 constexpr int kGatherTokens = 64;  // output tokens per gather block
 constexpr int kBig = 0x7FFFFFFF;
@@ -378,13 +378,18 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
     const uint64_t bg = __ballot(ge), bl = __ballot(le);
     const int A = rge + __popcll(bg & lt);
     const int lin = rle + __popcll(bl & le_m);
-    if (le) spos[tot_le - lin + 1] = (uint16_t)(wbeg + j * 64 + lane);
-    const bool cond = ge && (A + lin < tot_le);
-    nsw += __popcll(__ballot(cond));
-    const uint64_t bf = __ballot(ge && !cond);
-    if (bf && ff == kBig) ff = wbeg + j * 64 + (__ffsll((unsigned long long)bf) - 1);
+    const int pos = wbeg + j * 64 + lane;
+    if (le) spos[tot_le - lin + 1] = (uint16_t)pos;
+    const bool cond = A + lin < tot_le;
+    nsw += (ge && cond) ? 1 : 0;               // per lane; reduced once below
+    ff = (ge && !cond) ? min(ff, pos) : ff;
     rge += __popcll(bg);
     rle += __popcll(bl);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    nsw += __shfl_xor(nsw, o, 64);
+    ff = min(ff, __shfl_xor(ff, o, 64));
   }
   int msw, gnext;
   if constexpr (NW > 1) {
