@@ -31,3 +31,11 @@ if [ "$MODE" = "stamps" ]; then
   done
   cat gpurun_out/stamps.json
 fi
+if [ "$MODE" = "pmc" ]; then
+  cd /tmp && export TMPDIR=/tmp
+  for ctr in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 400 rocprofv3 --pmc $ctr --output-format csv -d "$R/gpurun_out/pmc_$ctr" -o run \
+        -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$R/gpurun_out/pmc_$ctr.log" 2>&1 || exit $?
+  done
+  find "$R/gpurun_out" -name "*counter_collection*" | head
+fi
