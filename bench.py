@@ -34,6 +34,19 @@ def algorithmic_bytes(es=2):
     return per_layer, score
 
 
+def pmc_traffic(kernel="kvc::score_kernel<1, 16>"):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
+    (profiles/r01_v5_pmc_traffic.json: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) measured
+    on this exact workload; None if absent."""
+    path = os.path.join(ROOT, "profiles", "r01_v5_pmc_traffic.json")
+    try:
+        with open(path) as f:
+            k = json.load(f)["kernels"][kernel]
+        return k["FETCH_bytes_x2_gfx950"] + k["WRITE_SIZE_bytes"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def cpu_baseline(seconds=12.0):
     """The reference's CPU op sequence (oracle/torch_port.py) on this host's cores, bounded."""
     from oracle.torch_port import fix_size_l2_layer
@@ -54,6 +67,42 @@ def cpu_baseline(seconds=12.0):
             "sample": f"{n} layers of fix_size_l2(512) on one [1,32,16384,128] bf16 layer "
                       f"(torch CPU ops: norm->argsort->sort->gather), {dt:.1f}s, "
                       f"{torch.backends.cpu.get_cpu_capability()}"}
+
+
+def timed_steps(step, steps, warmup, dist, sync, device, on_start=None):
+    """W untimed warmup steps, then exactly K timed steps bracketed by barrier + sync on both
+    sides; returns the MAX elapsed seconds over ranks (all ranks return the same value)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    if dist:
+        dist.barrier()
+    sync()
+    if on_start:
+        on_start()
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(steps):
+        out = step()
+    sync()
+    if dist:
+        dist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    del out
+    if dist:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def shard_layers(num_layers_total, world, rank):
+    """Contiguous layer block [start, end) owned by `rank` (layers sharded, no collectives)."""
+    per = num_layers_total // world
+    extra = num_layers_total % world
+    start = rank * per + min(rank, extra)
+    return start, start + per + (1 if rank < extra else 0)
 
 
 def main():
@@ -88,30 +137,11 @@ def main():
         return fix_size_l2_compress(layers, fix_kv_size=FIX, keep_ratio=0.0, strategy="keep_low",
                                     skip_layers=[])
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
     # per-kernel durations: the engine splits each launch into its three kernels with HIP
     # events (recorded on the stream they run on) for the whole timed region
     timer = _engine.PhaseTimer()
-    _engine.set_phase_timer(timer)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    del out
-    if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
+    elapsed = timed_steps(step, args.steps, args.warmup, dist, torch.cuda.synchronize, dev,
+                          on_start=lambda: _engine.set_phase_timer(timer))
     _engine.set_phase_timer(None)
     dur = timer.durations_ms()
 
@@ -121,6 +151,7 @@ def main():
         tokens = LAYERS * S * args.steps * world
         score_ms = sum(dur["score"]) / len(dur["score"])
         score_gbps = score_bytes_layer * LAYERS / (score_ms * 1e-3) / 1e9
+        traffic = pmc_traffic()
         path_gbps = per_layer * LAYERS / (ms_step * 1e-3) / 1e9
         res = {
             "metric": "KV tokens scored+evicted/sec at S=16384, fix_size=512; PPL delta vs ref",
@@ -142,7 +173,9 @@ def main():
                        "fix_kv_size": FIX, "parallelism": f"layers sharded x{world}, no collectives"},
             "roofline": {"bound": "hbm", "kernel": "score_kernel (key L2 norms)",
                          "achieved": score_gbps, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                         "frac": score_gbps / PEAK_HBM_GBPS, "traffic": None},
+                         "frac": score_gbps / PEAK_HBM_GBPS, "traffic": traffic,
+                         "algorithmic_bytes_per_launch": score_bytes_layer * LAYERS,
+                         "traffic_source": "profiles/r01_v5_pmc_traffic.json (rocprofv3 --pmc)"},
             "path_roofline": {"achieved": path_gbps, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                               "frac": path_gbps / PEAK_HBM_GBPS,
                               "bytes_per_layer": per_layer},

@@ -14,6 +14,17 @@ from .methods import (
     register_method,
     COMPRESS_METHODS,
 )
+from .evaluate import (
+    evaluate_with_compression,
+    evaluate_baseline,
+    compare_methods,
+)
+from .benchmark import (
+    benchmark,
+    measure_generation_metrics,
+    run_benchmark_suite,
+    print_benchmark_summary,
+)
 from .utils import (
     to_dynamic_cache,
     normalize_kv_cache,
@@ -25,6 +36,8 @@ from .utils import (
 __all__ = [
     "l2_compress", "fix_size_l2_compress", "streaming_llm_compress",
     "get_compress_fn", "list_methods", "register_method", "COMPRESS_METHODS",
+    "evaluate_with_compression", "evaluate_baseline", "compare_methods",
+    "benchmark", "measure_generation_metrics", "run_benchmark_suite", "print_benchmark_summary",
     "to_dynamic_cache", "normalize_kv_cache", "get_cache_size_mb", "get_cache_info",
     "get_seq_len",
 ]
