@@ -87,6 +87,15 @@ __device__ __forceinline__ typename DTypeTraits<DT>::key_t key_of(float f, bool 
   } while (0)
 #endif
 
+// threadIdx.x behind an opaque (volatile) move: values derived from it are recomputed where they
+// are used instead of being hoisted out of the fused kernel's persistent loop, where they would
+// stay live (and spill) through the register-hungry select code.
+__device__ __forceinline__ int opaque_tid() {
+  int t = (int)threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -117,35 +126,19 @@ __device__ __forceinline__ void accum_chunk(float (&acc)[8], const uint4 x, int 
   }
 }
 
+// One 64-token tile of one (layer, b, h) row: coalesced 16-B loads -> per-wave LDS slab ->
+// one lane per token, torch.norm's 8-accumulator FMA order.  `wl` is this wave's slab
+// (kTile * ROWB bytes).  sc1 = publish the norms write-through for an in-launch consumer.
 template <int DT, int NC>
-__global__ void __launch_bounds__(kScoreThreads)
-    score_kernel(const kvc_layer_t* __restrict__ L, int nl, int H, int64_t total_tiles,
-                 char* __restrict__ norms, int64_t norm_stride) {
+__device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int tt, int H,
+                                           char* wl, char* norms, int64_t norm_stride,
+                                           bool sc1) {
   constexpr int ESZ = DTypeTraits<DT>::esz;
   constexpr int CP = (NC % 8 == 0) ? 8 : 10;  // 16-B chunks per token per phase
   constexpr int NPH = NC / CP;
   constexpr int ROWB = CP * 16 + 16;  // padded LDS row: conflict-free ds_read_b128 per lane
-  __shared__ __attribute__((aligned(16))) char lds[kScoreWaves][kTile * ROWB];
-
   const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t g = (int64_t)blockIdx.x * kScoreWaves + wid;
-  if (g >= total_tiles) return;
-
-  int lo = 0, hi = nl - 1;  // largest layer with tile0 <= g
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (L[mid].tile0 <= g)
-      lo = mid;
-    else
-      hi = mid - 1;
-  }
-  const kvc_layer_t* ly = L + lo;
   const int zlen = ly->zone_len;
-  const int tpr = (zlen + kTile - 1) / kTile;
-  const int local = (int)(g - ly->tile0);
-  const int row = local / tpr;
-  const int tt = local - row * tpr;
   const int b = row / H, h = row - (row / H) * H;
   const int tok0 = tt * kTile;
   const int ntok = min(kTile, zlen - tok0);
@@ -153,8 +146,6 @@ __global__ void __launch_bounds__(kScoreThreads)
   const char* base = static_cast<const char*>(ly->k) +
                      ((int64_t)b * ly->k_stride[0] + (int64_t)h * ly->k_stride[1] +
                       (int64_t)(ly->zone_start + tok0) * ly->k_stride[2]) * ESZ;
-  char* wl = lds[wid];
-
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ph = 0; ph < NPH; ++ph) {
@@ -188,11 +179,46 @@ __global__ void __launch_bounds__(kScoreThreads)
     for (int j = 1; j < 8; ++j) s = s + acc[j];
     const float r = __builtin_sqrtf(s);
     char* nrow = norms + (int64_t)(ly->row0 + row) * norm_stride * ESZ;
-    if constexpr (DT == KVC_BF16)
-      reinterpret_cast<uint16_t*>(nrow)[tok0 + lane] = (uint16_t)f32_to_bf16_rne(r);
-    else
-      reinterpret_cast<float*>(nrow)[tok0 + lane] = r;
+    if constexpr (DT == KVC_BF16) {
+      uint16_t* d = reinterpret_cast<uint16_t*>(nrow) + tok0 + lane;
+      const uint16_t val = (uint16_t)f32_to_bf16_rne(r);
+      if (sc1)
+        __hip_atomic_store(d, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        *d = val;
+    } else {
+      float* d = reinterpret_cast<float*>(nrow) + tok0 + lane;
+      if (sc1)
+        __hip_atomic_store(d, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        *d = r;
+    }
   }
+}
+
+template <int DT, int NC>
+__global__ void __launch_bounds__(kScoreThreads)
+    score_kernel(const kvc_layer_t* __restrict__ L, int nl, int H, int64_t total_tiles,
+                 char* __restrict__ norms, int64_t norm_stride) {
+  constexpr int CP = (NC % 8 == 0) ? 8 : 10;
+  constexpr int ROWB = CP * 16 + 16;
+  __shared__ __attribute__((aligned(16))) char lds[kScoreWaves][kTile * ROWB];
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t g = (int64_t)blockIdx.x * kScoreWaves + wid;
+  if (g >= total_tiles) return;
+  int lo = 0, hi = nl - 1;  // largest layer with tile0 <= g
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (L[mid].tile0 <= g)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  const kvc_layer_t* ly = L + lo;
+  const int tpr = (ly->zone_len + kTile - 1) / kTile;
+  const int local = (int)(g - ly->tile0);
+  const int row = local / tpr;
+  score_tile<DT, NC>(ly, row, local - row * tpr, H, lds[wid], norms, norm_stride, false);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -207,6 +233,9 @@ struct SelScalars {
   float fmax[kSelWaves];
   int fnan[kSelWaves];
 };
+
+template <typename KeyT>
+constexpr int kSelLdsBytes = kZoneMax * (int)sizeof(KeyT) + kZoneMax * 2 + (kZoneMax + 8) * 2;
 
 __device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
 __device__ __forceinline__ uint64_t lanemask_le(int lane) {
@@ -523,38 +552,35 @@ __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, SelScalars<Ke
   }
 }
 
-template <int DT>
-__global__ void __launch_bounds__(kSelThreads)
-    select_kernel(const kvc_layer_t* __restrict__ L, int BH, int order, int algo,
-                  const char* __restrict__ norms, int64_t norm_stride,
-                  int32_t* __restrict__ out_idx, int64_t idx_stride, int wave_seg,
-                  uint64_t* stamps) {
+// Reference-exact selection for one (layer, b, h) row whose zone norms are at `nrow`; LDS in
+// `smem` (key | idx | spos, see select_kernel) and `sc`.  Emits the kept zone-local indices in
+// ascending order to `out` (global int32) or, with TO_LDS, to `sel` (LDS u16, may alias
+// the key region: keys are dead by then).
+template <int DT, bool TO_LDS>
+__device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, int order, int algo,
+                            const char* __restrict__ nrow, int32_t* out, uint16_t* sel,
+                            char* smem, SelScalars<typename DTypeTraits<DT>::key_t>& sc,
+                            int wave_seg, uint64_t* stamps) {
   typedef typename DTypeTraits<DT>::key_t KeyT;
   constexpr int ESZ = DTypeTraits<DT>::esz;
-  // LDS: key[kZoneMax] | idx[kZoneMax] (u16) | spos[kZoneMax + 8] (u16) | scalars
   constexpr int KEY_B = kZoneMax * (int)sizeof(KeyT);
   constexpr int IDX_B = kZoneMax * 2;
-  constexpr int SPOS_B = (kZoneMax + 8) * 2;
-  __shared__ __attribute__((aligned(16))) char smem[KEY_B + IDX_B + SPOS_B];
-  __shared__ SelScalars<KeyT> sc;
   KeyT* key = reinterpret_cast<KeyT*>(smem);
   uint16_t* idx = reinterpret_cast<uint16_t*>(smem + KEY_B);
   uint16_t* spos = reinterpret_cast<uint16_t*>(smem + KEY_B + IDX_B);
-
-  const int row = blockIdx.x;
   KVC_STAMP(0);
-  const kvc_layer_t* ly = L + row / BH;
   const int n = ly->zone_len;
   const int k = ly->n_select;
   if (k <= 0 || n <= 0 || n > kZoneMax) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  int32_t* out = out_idx + (int64_t)row * idx_stride;
   if (k >= n) {  // keep everything (e.g. h2o_l2 when the middle is no longer than heavy_hitter)
-    for (int i = tid; i < n; i += kSelThreads) out[i] = i;
+    for (int i = tid; i < n; i += kSelThreads) {
+      if constexpr (TO_LDS) sel[i] = (uint16_t)i;
+      else out[i] = i;
+    }
     return;
   }
   const bool desc = order == KVC_DESC;
-  const char* nrow = norms + (int64_t)row * norm_stride * ESZ;
 
   // ---- keys ----
   if (ly->score_mode == KVC_SCORE_SNAPKV) {
@@ -658,10 +684,31 @@ __global__ void __launch_bounds__(kSelThreads)
   for (int j = 0; j < J; ++j) {
     const bool f = (fm >> j) & 1u;
     const uint64_t bf = __ballot(f);
-    if (f) out[run + __popcll(bf & lanemask_lt(lane))] = wbeg + j * 64 + lane;
+    if (f) {
+      const int r = run + __popcll(bf & lanemask_lt(lane));
+      if constexpr (TO_LDS) sel[r] = (uint16_t)(wbeg + j * 64 + lane);
+      else out[r] = wbeg + j * 64 + lane;
+    }
     run += __popcll(bf);
   }
   KVC_STAMP(4);
+}
+
+
+template <int DT>
+__global__ void __launch_bounds__(kSelThreads)
+    select_kernel(const kvc_layer_t* __restrict__ L, int BH, int order, int algo,
+                  const char* __restrict__ norms, int64_t norm_stride,
+                  int32_t* __restrict__ out_idx, int64_t idx_stride, int wave_seg,
+                  uint64_t* stamps) {
+  typedef typename DTypeTraits<DT>::key_t KeyT;
+  constexpr int ESZ = DTypeTraits<DT>::esz;
+  // LDS: key[kZoneMax] | idx[kZoneMax] (u16) | spos[kZoneMax + 8] (u16) | scalars
+  __shared__ __attribute__((aligned(16))) char smem[kSelLdsBytes<KeyT>];
+  __shared__ SelScalars<KeyT> sc;
+  const int row = blockIdx.x;
+  select_body<DT, false>(L + row / BH, order, algo, norms + (int64_t)row * norm_stride * ESZ,
+                  out_idx + (int64_t)row * idx_stride, nullptr, smem, sc, wave_seg, stamps);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -734,51 +781,214 @@ __global__ void __launch_bounds__(kGatherThreads)
   }
 }
 
-// Experimental SCORE variant (KVC_SCORE_VARIANT=direct): each lane streams its own token row
-// with 16-B loads straight to registers (no LDS transpose); one wave instruction then touches
-// 64 rows.  Kept to measure whether a fused per-row design can skip the LDS slab.
-template <int DT, int NC>
-__global__ void __launch_bounds__(kScoreThreads)
-    score_direct_kernel(const kvc_layer_t* __restrict__ L, int nl, int H, int64_t total_tiles,
-                        char* __restrict__ norms, int64_t norm_stride) {
-  constexpr int ESZ = DTypeTraits<DT>::esz;
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t g = (int64_t)blockIdx.x * kScoreWaves + wid;
-  if (g >= total_tiles) return;
+// ---------------------------------------------------------------------------------------------
+// FUSED persistent kernel: score, select and gather of a whole call in one launch
+// ---------------------------------------------------------------------------------------------
+// One 1024-thread workgroup per CU.  Each workgroup takes an arrival ticket; the first
+// `n_score_first` arrivals start as SCORE workgroups, the rest go straight to the ROW queue.
+//   SCORE: score wave w (of n_score_first * 16) takes chunks w, w + W, ... of 4 consecutive
+//     64-position tiles (the global layer-major tile order of kvc_plan), computes their norms
+//     (score_tile, write-through stores), drains (`s_waitcnt vmcnt(0)`) and sets the chunk's
+//     per-tile flags with plain write-through stores.  (Agent-scope atomics here cost ~8% of
+//     the stream: a pending atomic makes the wave's next load wait for it.)  Then the
+//     workgroup joins the ROW queue.
+//   ROW: rows are dequeued in layer-major order (the next ticket is fetched while a row runs);
+//     a selecting row polls its tile flags (one load per thread, __syncthreads_and, s_sleep),
+//     then one agent-scope acquire (L1 invalidate), a barrier, select into LDS, gather; a
+//     copy-only row is gathered at once.
+// Progress is guaranteed: tickets are sequential, so once any workgroup is on the ROW queue
+// every SCORE workgroup is resident, and SCORE waves never wait.  Spins are bounded anyway
+// (ctl[kCtlError] = 1).  While the ROW workgroups select (LDS/issue-bound) the SCORE
+// workgroups keep HBM streaming -- the reason to fuse.  (cdna_hip_programming.md §6
+// Guideline 16 for the publish / acquire protocol.)
+constexpr int kChunkTiles = 4;
+// tuning timeline (diag & 2): s_memrealtime (100 MHz, chip-wide) stamps into the idle index region
+#define KVC_TL(slot)                                                   \
+  do {                                                                 \
+    if ((diag & 2) && tid == 0) tl[slot] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+constexpr int kCtlHeader = 32;  // ints before the per-row counters
+constexpr int kCtlTicket = 0, kCtlError = 1, kCtlRowQ = 2;
+
+__host__ __device__ __forceinline__ bool fused_selects(const kvc_layer_t& y) {
+  return y.n_select > 0 && y.n_select < y.zone_len;
+}
+
+// layer of global score tile g: the largest l with L[l].tile0 <= g (copy-only layers own no
+// tiles and share tile0 with the next layer, so they are never the largest such l for g < total)
+__device__ __forceinline__ const kvc_layer_t* tile_layer(const kvc_layer_t* L, int nl, int g) {
   int lo = 0, hi = nl - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
     if (L[mid].tile0 <= g) lo = mid; else hi = mid - 1;
   }
-  const kvc_layer_t* ly = L + lo;
-  const int zlen = ly->zone_len;
-  const int tpr = (zlen + kTile - 1) / kTile;
-  const int local = (int)(g - ly->tile0);
-  const int row = local / tpr;
-  const int tt = local - row * tpr;
-  const int b = row / H, h = row - (row / H) * H;
-  const int tok0 = tt * kTile;
-  const int ntok = min(kTile, zlen - tok0);
-  if (lane >= ntok) return;
-  const char* p = static_cast<const char*>(ly->k) +
-                  ((int64_t)b * ly->k_stride[0] + (int64_t)h * ly->k_stride[1] +
-                   (int64_t)(ly->zone_start + tok0 + lane) * ly->k_stride[2]) * ESZ;
-  uint4 x[NC];
+  return L + lo;
+}
+
+// Copy one output row (sink ++ selected ++ tail) of K and V with the whole workgroup.
+// sel: ascending zone-local kept indices in LDS, or nullptr when no selection ran.
+template <int DT, int NC>
+__device__ __forceinline__ void gather_row(const kvc_layer_t* __restrict__ ly, int r, int H,
+                                           const uint16_t* sel) {
+  constexpr int ESZ = DTypeTraits<DT>::esz;
+  constexpr int BATCH = 4;
+  const int n_out = ly->n_out;
+  const int nu = n_out * NC;
+  const int b = r / H, h = r - (r / H) * H;
+  const int sink = ly->sink_len, nsel = ly->n_select;
+  const char* kb = static_cast<const char*>(ly->k) +
+                   ((int64_t)b * ly->k_stride[0] + (int64_t)h * ly->k_stride[1]) * ESZ;
+  const char* vb = static_cast<const char*>(ly->v) +
+                   ((int64_t)b * ly->v_stride[0] + (int64_t)h * ly->v_stride[1]) * ESZ;
+  const int64_t kss = ly->k_stride[2] * ESZ, vss = ly->v_stride[2] * ESZ;
+  char* ko = static_cast<char*>(ly->k_out) + (int64_t)r * nu * 16;
+  char* vo = static_cast<char*>(ly->v_out) + (int64_t)r * nu * 16;
+  const int tid0 = opaque_tid();
+  for (int u0 = 0; u0 < nu; u0 += kSelThreads * BATCH) {
+    uint4 xk[BATCH], xv[BATCH];
+    bool gat[BATCH];
 #pragma unroll
-  for (int c = 0; c < NC; ++c) x[c] = *reinterpret_cast<const uint4*>(p + c * 16);
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < BATCH; ++i) {
+      const int u = u0 + tid0 + i * kSelThreads;
+      gat[i] = false;
+      if (u < nu) {
+        const int t = u / NC, c = u - (u / NC) * NC;
+        int src;
+        if (t < sink) {
+          src = t;
+        } else if (t < sink + nsel) {
+          int zi = sel ? (int)sel[t - sink] : t - sink;
+          zi = min(max(zi, 0), ly->zone_len - 1);
+          src = ly->zone_start + zi;
+          gat[i] = true;
+        } else {
+          src = ly->tail_start + (t - sink - nsel);
+        }
+        xk[i] = *reinterpret_cast<const uint4*>(kb + src * kss + c * 16);
+        xv[i] = *reinterpret_cast<const uint4*>(vb + src * vss + c * 16);
+      }
+    }
 #pragma unroll
-  for (int c = 0; c < NC; ++c) accum_chunk<DT, NC>(acc, x[c], c);
-  float s = acc[0];
-#pragma unroll
-  for (int j = 1; j < 8; ++j) s = s + acc[j];
-  const float r = __builtin_sqrtf(s);
-  char* nrow = norms + (int64_t)(ly->row0 + row) * norm_stride * ESZ;
-  if constexpr (DT == KVC_BF16)
-    reinterpret_cast<uint16_t*>(nrow)[tok0 + lane] = (uint16_t)f32_to_bf16_rne(r);
-  else
-    reinterpret_cast<float*>(nrow)[tok0 + lane] = r;
+    for (int i = 0; i < BATCH; ++i) {
+      const int u = u0 + tid0 + i * kSelThreads;
+      if (u < nu) {
+        uint4 a = xk[i], q = xv[i];
+        if constexpr (DT == KVC_BF16) {
+          if (gat[i]) {
+            a.x = canon_nan_bf16x2(a.x); a.y = canon_nan_bf16x2(a.y);
+            a.z = canon_nan_bf16x2(a.z); a.w = canon_nan_bf16x2(a.w);
+            q.x = canon_nan_bf16x2(q.x); q.y = canon_nan_bf16x2(q.y);
+            q.z = canon_nan_bf16x2(q.z); q.w = canon_nan_bf16x2(q.w);
+          }
+        }
+        *reinterpret_cast<uint4*>(ko + (int64_t)u * 16) = a;
+        *reinterpret_cast<uint4*>(vo + (int64_t)u * 16) = q;
+      }
+    }
+  }
+}
+
+template <int DT, int NC>
+__global__ void __launch_bounds__(kSelThreads)
+    fused_kernel(const kvc_layer_t* __restrict__ L, int nl, int H, int BH, int order, int algo,
+                 char* __restrict__ norms, int64_t norm_stride, int* __restrict__ ctl,
+                 int wave_seg, int total_tiles, int rows, int n_score_first, int diag,
+                 uint64_t* __restrict__ tl) {
+  typedef typename DTypeTraits<DT>::key_t KeyT;
+  constexpr int ESZ = DTypeTraits<DT>::esz;
+  static_assert(NC == 8 || NC == 16, "fused path: 128/256-byte rows");
+  constexpr int ROWB = 8 * 16 + 16;
+  constexpr int SCORE_B = kSelWaves * kTile * ROWB;
+  constexpr int SEL_B = kSelLdsBytes<KeyT>;
+  constexpr int SM_B = SCORE_B > SEL_B ? SCORE_B : SEL_B;
+  __shared__ __attribute__((aligned(16))) char smem[SM_B];
+  __shared__ SelScalars<KeyT> sc;
+  __shared__ int sh_val;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  int* tile_flag = ctl + kCtlHeader;
+  if (tid == 0)
+    sh_val = __hip_atomic_fetch_add(ctl + kCtlTicket, 1, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int ticket = __builtin_amdgcn_readfirstlane(sh_val);
+  __syncthreads();
+  KVC_TL(rows * 4 + ticket * 2);
+
+  if (ticket < n_score_first) {  // ---- SCORE: static chunk striding over the score waves ----
+    char* wl = smem + wid * kTile * ROWB;
+    const int nchunks = (total_tiles + kChunkTiles - 1) / kChunkTiles;
+    const int nsw = n_score_first * kSelWaves;
+    for (int claim = ticket * kSelWaves + wid; claim < nchunks; claim += nsw) {
+      const int g0 = claim * kChunkTiles;
+      const int ng = min(kChunkTiles, total_tiles - g0);
+      for (int i = 0; i < ng; ++i) {
+        const int g = g0 + i;
+        const kvc_layer_t* ly = tile_layer(L, nl, g);
+        const int tpr = (ly->zone_len + kTile - 1) / kTile;
+        const int local = g - ly->tile0;
+        const int row = local / tpr;
+        score_tile<DT, NC>(ly, row, local - row * tpr, H, wl, norms, norm_stride, true);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // norms reach L2 before the flags
+      if (lane < ng)
+        __hip_atomic_store(tile_flag + g0 + lane, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (diag & 5) return;  // tuning: score phase alone (4: on the cus - nsel score workgroups)
+  __syncthreads();
+  KVC_TL(rows * 4 + ticket * 2 + 1);
+
+  // ---- ROW queue: select + gather; the next row's ticket is fetched while this one runs ----
+  if (tid == 0)
+    sh_val = __hip_atomic_fetch_add(ctl + kCtlRowQ, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  int r = __builtin_amdgcn_readfirstlane(sh_val);
+  __syncthreads();
+  int next = 0;
+  while (r < rows) {
+    if (tid == 0)
+      next = __hip_atomic_fetch_add(ctl + kCtlRowQ, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    KVC_TL(r * 4);
+    const int l = r / BH;
+    const kvc_layer_t* ly = L + l;
+    const int row = r - l * BH;
+    if (fused_selects(*ly)) {
+      const int tpr = (ly->zone_len + kTile - 1) / kTile;
+      const int* f = tile_flag + ly->tile0 + row * tpr;
+      for (int spins = 0;; ++spins) {  // every tile of the row flagged?
+        int ok = 1;
+        for (int t = tid; t < tpr; t += kSelThreads)
+          ok &= __hip_atomic_load(f + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__syncthreads_and(ok)) break;
+        if (spins > (1 << 22)) {
+          if (tid == 0)
+            __hip_atomic_store(ctl + kCtlError, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+      }
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+      KVC_TL(r * 4 + 1);
+      uint16_t* sel = reinterpret_cast<uint16_t*>(smem);  // key region, dead after the chain
+      select_body<DT, true>(ly, order, algo, norms + (int64_t)r * norm_stride * ESZ, nullptr,
+                            sel, smem, sc, wave_seg, nullptr);
+      __syncthreads();
+      KVC_TL(r * 4 + 2);
+      gather_row<DT, NC>(ly, row, H, sel);
+    } else {
+      gather_row<DT, NC>(ly, row, H, nullptr);
+    }
+    if (tid == 0) sh_val = next;
+    __syncthreads();  // LDS and sh_val are reused by the next row
+    KVC_TL(r * 4 + 3);
+    r = __builtin_amdgcn_readfirstlane(sh_val);
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -850,6 +1060,8 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
     info->norm_row_stride = (int64_t)round_up((size_t)max_zone, kTile);
     info->index_row_stride = (int64_t)round_up((size_t)(max_sel > 0 ? max_sel : 1), 16);
     size_t off = 0;
+    info->control_offset = off;  // fused kernel: tickets, error flag, row queue, tile flags
+    off = round_up(off + (size_t)(kCtlHeader + tiles) * 4, 256);
     info->desc_offset = off;
     off = round_up(off + (size_t)nl * sizeof(kvc_layer_t), 256);
     info->norm_offset = off;
@@ -868,13 +1080,8 @@ template <int DT, int NC>
 static void launch_score(const kvc_layer_t* Ld, int nl, int H, int64_t tiles, char* norms,
                          int64_t nstride, hipStream_t s) {
   const unsigned grid = (unsigned)((tiles + kScoreWaves - 1) / kScoreWaves);
-  const char* var = getenv("KVC_SCORE_VARIANT");
-  if (var && strcmp(var, "direct") == 0)
-    hipLaunchKernelGGL((score_direct_kernel<DT, NC>), dim3(grid), dim3(kScoreThreads), 0, s, Ld,
-                       nl, H, tiles, norms, nstride);
-  else
-    hipLaunchKernelGGL((score_kernel<DT, NC>), dim3(grid), dim3(kScoreThreads), 0, s, Ld, nl, H,
-                       tiles, norms, nstride);
+  hipLaunchKernelGGL((score_kernel<DT, NC>), dim3(grid), dim3(kScoreThreads), 0, s, Ld, nl, H,
+                     tiles, norms, nstride);
 }
 
 // `work` = max n_out over layers; grid = (rows, token blocks)
@@ -972,6 +1179,46 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
   uint64_t* stamps = nullptr;
 #endif
   (void)hipGetLastError();
+  // Fused persistent path: all phases, no caller-provided indices, 128/256-byte rows (wider
+  // rows need more than the 128 VGPRs a 1024-thread workgroup allows).  KVC_FUSED=0 forces the
+  // three-kernel path (A/B comparisons, tests).
+  bool fused = p->phases == KVC_PHASE_ALL && !p->external_index && (nc == 8 || nc == 16);
+  if (const char* e = getenv("KVC_FUSED")) fused = fused && strcmp(e, "0") != 0;
+  if (fused) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      return KVC_E_HIP;
+    int* ctl = reinterpret_cast<int*>(w + info.control_offset);
+    if (hipMemsetAsync(ctl, 0, (size_t)(kCtlHeader + info.score_tiles) * 4, s) != hipSuccess)
+      return KVC_E_HIP;
+    // Workgroups that start on the ROW queue: enough select throughput to keep pace with the
+    // key stream (select ~7 cycles/position/CU vs ~24 (256-B rows) or ~12 (128-B rows) cycles
+    // of HBM share per position per CU); KVC_SEL_WGS overrides.
+    int nsel = (int)(cus * (nc == 16 ? 0.22 : 0.36) + 0.5);
+    if (const char* e = getenv("KVC_SEL_WGS")) nsel = atoi(e);
+    if (nsel < 1) nsel = 1;
+    if (nsel > cus - 1) nsel = cus - 1;
+    int diag = 0;  // tuning only: 1 = score phase alone (output incomplete)
+    if (const char* e = getenv("KVC_FUSED_DIAG")) diag = atoi(e);
+    const int n_score_first = info.score_tiles > 0 ? cus - ((diag & 1) ? 0 : nsel) : 0;
+    uint64_t* tl = reinterpret_cast<uint64_t*>(idx);
+    if ((diag & 2) && (size_t)info.rows * info.index_row_stride * 4 < (size_t)(info.rows * 4 + 2 * cus) * 8)
+      diag &= ~2;
+    const dim3 grid((unsigned)cus), block(kSelThreads);
+#define KVC_FUSED_LAUNCH(DT_, NC_)                                                             \
+  hipLaunchKernelGGL((fused_kernel<DT_, NC_>), grid, block, 0, s, layers_dev, nl, H, BH,       \
+                     p->order, p->algo, norms, info.norm_row_stride, ctl, wave_seg,             \
+                     (int)info.score_tiles, (int)info.rows, n_score_first, diag, tl)
+    if (p->dtype == KVC_BF16) {
+      if (nc == 8) { KVC_FUSED_LAUNCH(KVC_BF16, 8); } else { KVC_FUSED_LAUNCH(KVC_BF16, 16); }
+    } else {
+      if (nc == 8) { KVC_FUSED_LAUNCH(KVC_F32, 8); } else { KVC_FUSED_LAUNCH(KVC_F32, 16); }
+    }
+#undef KVC_FUSED_LAUNCH
+    return hipGetLastError() == hipSuccess ? KVC_OK : KVC_E_HIP;
+  }
   if ((p->phases & KVC_PHASE_SCORE) && info.score_tiles > 0 && !p->external_index) {
     if (p->dtype == KVC_BF16)
       dispatch_nc<KVC_BF16>(nc, true, layers_dev, nl, H, BH, info.score_tiles, norms,

@@ -42,12 +42,16 @@ _SUPPORTED = {torch.bfloat16: N.KVC_BF16, torch.float32: N.KVC_F32}
 
 
 class PhaseTimer:
-    """When installed with set_phase_timer(), every engine launch is split into its SCORE /
-    SELECT / GATHER kernels with HIP events (torch.cuda.Event, recorded on the stream the
-    kernels run on) around each, so per-kernel durations can be measured live (bench.py)."""
+    """When installed with set_phase_timer(), every engine launch is bracketed by HIP events
+    (torch.cuda.Event, recorded on the stream the kernels run on) so kernel durations can be
+    measured live (bench.py).  split=True additionally launches the SCORE / SELECT / GATHER
+    phases separately (three-kernel path) and times each; split=False times the launch as
+    issued ("all": the fused persistent kernel when it applies)."""
 
-    def __init__(self):
+    def __init__(self, split=True, keep_workspace=False):
+        self.split = split
         self.records = []
+        self.workspaces = [] if keep_workspace else None  # (ws, info) of each launch (tools)
 
     def durations_ms(self):
         torch.cuda.synchronize()
@@ -123,7 +127,7 @@ def _launch(params, table, ws, info, stream, phases):
     dev_tbl = ws.data_ptr() + int(info.desc_offset)
     saved = params.phases
     steps = ((("score", N.PHASE_SCORE), ("select", N.PHASE_SELECT), ("gather", N.PHASE_GATHER))
-             if _timer is not None else (("all", phases),))
+             if _timer is not None and _timer.split else (("all", phases),))
     for name, bits in steps:
         if not phases & bits:
             continue
@@ -178,5 +182,7 @@ def _run_group(device, dtype, B, H, D, js, out_list, order, algo):
         p = params()
         ws, info = _upload(p, table, device, js, B, H)
         _launch(p, table, ws, info, torch.cuda.current_stream(device), p.phases)
+        if _timer is not None and _timer.workspaces is not None:
+            _timer.workspaces.append((ws, info))
     for j, (ko, vo) in zip(js, outs):
         out_list[j.layer_idx] = (ko, vo)

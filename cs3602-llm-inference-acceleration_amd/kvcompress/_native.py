@@ -39,7 +39,8 @@ class Params(ctypes.Structure):
 
 
 class PlanInfo(ctypes.Structure):
-    _fields_ = [("desc_offset", ctypes.c_size_t), ("norm_offset", ctypes.c_size_t),
+    _fields_ = [("control_offset", ctypes.c_size_t),
+                ("desc_offset", ctypes.c_size_t), ("norm_offset", ctypes.c_size_t),
                 ("index_offset", ctypes.c_size_t), ("workspace_bytes", ctypes.c_size_t),
                 ("norm_row_stride", ctypes.c_int64), ("index_row_stride", ctypes.c_int64),
                 ("rows", ctypes.c_int64), ("score_tiles", ctypes.c_int64),

@@ -21,7 +21,8 @@
  * -> cat); the engine reproduces their results bit-exactly, including libstdc++'s introsort /
  * introselect tie order, torch.norm's 8-lane FMA order, and torch.gather's bf16 NaN rewrite.
  *
- * Phases (one HIP kernel each, all stream-ordered on `stream`):
+ * Phases (stream-ordered on `stream`; for KVC_PHASE_ALL with 8/16/32 16-byte chunks per row
+ * they run as ONE persistent kernel that overlaps selection with key streaming):
  *   SCORE  : key L2 norms of every zone token           -> workspace norm region
  *   SELECT : per (layer,b,h) row: snapkv scoring (opt.), reference-exact k-selection,
  *            ascending zone-local indices                -> workspace index region (int32)
@@ -109,6 +110,7 @@ typedef struct kvc_params {
 } kvc_params_t;
 
 typedef struct kvc_plan_info {
+  size_t control_offset;   /* workspace byte offset of the fused kernel's control words   */
   size_t desc_offset;      /* workspace byte offset of the device copy of the layer table */
   size_t norm_offset;      /* workspace byte offset of the norm region                    */
   size_t index_offset;     /* workspace byte offset of the int32 index region             */

@@ -30,7 +30,7 @@ def test_struct_layout():
     L = N.lib()
     assert L.kvc_layer_struct_size() == N.LAYER_DTYPE.itemsize == 136
     assert ctypes.sizeof(N.Params) == 32
-    assert ctypes.sizeof(N.PlanInfo) == 72
+    assert ctypes.sizeof(N.PlanInfo) == 80
     assert L.kvc_version() == 1
     assert L.kvc_max_zone_len() == 16384
 

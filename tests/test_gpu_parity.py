@@ -26,8 +26,16 @@ def _run_case(case, values):
     return tin, out
 
 
+@pytest.fixture(params=["fused", "kernels"])
+def launch_path(request, monkeypatch):
+    """Both launch paths of kvc_launch: the fused persistent kernel (default for 128/256-byte
+    rows) and the three-kernel SCORE/SELECT/GATHER path (KVC_FUSED=0)."""
+    monkeypatch.setenv("KVC_FUSED", "1" if request.param == "fused" else "0")
+    return request.param
+
+
 @pytest.mark.parametrize("cid", fixtures.case_ids())
-def test_engine_matches_reference_golden(cid):
+def test_engine_matches_reference_golden(cid, launch_path):
     case = fixtures.get_case(cid)
     if case["error"]:
         with pytest.raises(Exception) as ei:
@@ -161,7 +169,7 @@ def test_dynamic_cache_input():
         assert np.array_equal(to_np(ko), rk) and np.array_equal(to_np(vo), rv)
 
 
-def test_headline_geometry_32_layers():
+def test_headline_geometry_32_layers(launch_path):
     """BASELINE headline: 32 layers of [1,32,16384,128] bf16, fix_size_l2(512) in ONE call;
     two sampled layers checked bit-exactly against the oracle."""
     from kvcompress.methods import fix_size_l2_compress

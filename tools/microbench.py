@@ -11,8 +11,10 @@ sys.path.insert(0, os.path.join(ROOT, "cs3602-llm-inference-acceleration_amd"))
 from kvcompress import _engine  # noqa: E402
 from kvcompress.methods import fix_size_l2_compress  # noqa: E402
 
-# variant = "<score kernel>:<pipeline chunks>", e.g. lds:1,lds:4
-variants = sys.argv[1].split(",") if len(sys.argv) > 1 else ["lds:1", "lds:4"]
+# variant = split | unfused | fused[@W]:  split = three kernels timed per phase; unfused = three
+# kernels timed as one launch (KVC_FUSED=0); fused = the persistent kernel (one launch), @W =
+# W workgroups start on the row queue (KVC_SEL_WGS)
+variants = sys.argv[1].split(",") if len(sys.argv) > 1 else ["split", "unfused", "fused"]
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(0)
@@ -23,10 +25,15 @@ res = {v: {} for v in variants}
 ref = None
 for r in range(rounds):
     for v in variants:
-        kern, chunks = (v.split(":") + ["1"])[:2]
-        os.environ["KVC_SCORE_VARIANT"] = kern
-        os.environ["KVC_PIPELINE_CHUNKS"] = chunks
-        t = _engine.PhaseTimer()
+        name, _, diag = v.partition("#")
+        name, _, wgs = name.partition("@")
+        os.environ["KVC_FUSED_DIAG"] = diag or "0"
+        os.environ["KVC_FUSED"] = "1" if name == "fused" else "0"
+        if wgs:
+            os.environ["KVC_SEL_WGS"] = wgs
+        else:
+            os.environ.pop("KVC_SEL_WGS", None)
+        t = _engine.PhaseTimer(split=(v == "split"))
         _engine.set_phase_timer(t)
         torch.cuda.synchronize()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -40,7 +47,9 @@ for r in range(rounds):
         d["step_wall"] = [a.elapsed_time(b) / 5]
         for ph, xs in d.items():
             res[v].setdefault(ph, []).append(min(xs))
-        if ref is None:
+        if diag:
+            pass
+        elif ref is None:
             ref = [(a.clone(), b.clone()) for a, b in out]
         else:
             assert all(torch.equal(a, c) and torch.equal(b, e) for (a, b), (c, e) in zip(out, ref))
