@@ -79,7 +79,7 @@ __device__ __forceinline__ typename DTypeTraits<DT>::key_t key_of(float f, bool 
 #ifdef KVC_STAMPS
 #define KVC_STAMP(i)                                                             \
   do {                                                                           \
-    if (stamps && threadIdx.x == 0) stamps[blockIdx.x * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+    if (stamps && threadIdx.x == 0) stamps[blockIdx.x * 32 + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
 #define KVC_STAMP(i) \
@@ -226,16 +226,19 @@ __global__ void __launch_bounds__(kScoreThreads)
 // ---------------------------------------------------------------------------------------------
 template <typename KeyT>
 struct SelScalars {
-  int m[2];      // swap count of the current partition (double-buffered by level parity)
-  int gnext[2];  // g_{m+1}: first "not less than pivot" position that is not swapped
-  int wa[kSelWaves];
-  int wb[kSelWaves];
+  int wa[kSelWaves];  // per wave: ge count | le count << 16 (P1); snapkv scratch
+  int wb[kSelWaves];  //           snapkv scratch
+  int wm[kSelWaves];  //           swaps | first unswapped ge position << 16 (P2)
   float fmax[kSelWaves];
   int fnan[kSelWaves];
 };
 
+// rank -> position tables (1-based); the last 64 entries of each are per-lane sinks for the
+// stores of lanes that have nothing to record (branch-free scatter)
+constexpr int kSposLen = kZoneMax + 8 + 64;     // s ranks (<= n)
+constexpr int kGposLen = kZoneMax / 2 + 8 + 64; // g ranks of the m <= (n-1)/2 swapped ge
 template <typename KeyT>
-constexpr int kSelLdsBytes = kZoneMax * (int)sizeof(KeyT) + kZoneMax * 2 + (kZoneMax + 8) * 2;
+constexpr int kSelLdsBytes = kZoneMax * (int)sizeof(KeyT) + kZoneMax * 2 + (kSposLen + kGposLen) * 2;
 
 __device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
 __device__ __forceinline__ uint64_t lanemask_le(int lane) {
@@ -332,25 +335,48 @@ __device__ __forceinline__ void group_sync() {
 #define KVC_TICK(v) (void)0
 #endif
 
-// One partition level over [lo, hi) with at most JM positions per lane (compile-time, so the
-// passes are branch-free straight-line code).  Returns cut.  See run_chain for the algorithm.
+// Uniform (wave-invariant) value into an SGPR, so that the arithmetic on it runs on the scalar
+// unit instead of costing a 4-cycle wave64 VALU slot in every wave.
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+// inclusive prefix sum within each 16-lane row (4 DPP adds); lanes 0..15 = the 16 waves
+__device__ __forceinline__ int row_scan16(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);  // row_shr:8
+  return v;
+}
+// lanes below this one with their bit set in `mask`, plus `base` (v_mbcnt_lo/hi: 2 VALU)
+__device__ __forceinline__ int mbcnt(uint64_t mask, int base) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, (uint32_t)base));
+}
+
+// One partition level over [lo, hi) with at most JM positions per lane (compile-time bound; the
+// passes stop at the segment's own J with a scalar branch).  Returns cut.  See run_chain for
+// the algorithm.  The level is issue-bound (every wave executes its bookkeeping), so all
+// wave-uniform work -- median of 3, cross-wave prefix sums, swap count, g_{m+1} -- runs on
+// SGPRs (readfirstlane / readlane / ballot popcounts) and per-position work is ~30 VALU per
+// 64 positions.
 template <typename KeyT, int NT, int JM>
 __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_t* spos,
-                                               SelScalars<KeyT>& sc, int lo, int hi, int par,
+                                               SelScalars<KeyT>& sc, int lo, int hi,
                                                uint64_t* acc) {
   constexpr int NW = NT / 64;
+  uint16_t* gpos = spos + kSposLen;
   const int lane = threadIdx.x & 63;
-  const int wid = (NT == 64) ? 0 : (int)(threadIdx.x >> 6);
+  const int wid = (NT == 64) ? 0 : uni((int)(threadIdx.x >> 6));
   const int tid = wid * 64 + lane;
-  const uint64_t lt = lanemask_lt(lane), le_m = lanemask_le(lane);
   uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
   KVC_TICK(t0);
   const int J = (hi - lo - 1 + NT - 1) / NT;  // <= JM
   const int wbeg = lo + 1 + wid * J * 64;
-  // ---- loads first: median candidates, the pivot slot and this lane's keys ----
+  const int pos0 = wbeg + lane;
+  // ---- median of 3 (std::__move_median_to_first), on the scalar unit; the swap into lo is
+  // virtual until P2 ----
   const int a = lo + 1, b = lo + (hi - lo) / 2, c = hi - 1;
-  const KeyT ka = key[a], kb = key[b], kc = key[c], klo = key[lo];
-  // std::__move_median_to_first, evaluated by every lane; the swap into lo stays virtual
+  const uint32_t ka = (uint32_t)uni((int)key[a]), kb = (uint32_t)uni((int)key[b]);
+  const uint32_t kc = (uint32_t)uni((int)key[c]), klo = (uint32_t)uni((int)key[lo]);
   int ch;
   if (ka < kb) {
     if (kb < kc) ch = b; else if (ka < kc) ch = c; else ch = a;
@@ -361,117 +387,101 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
   } else {
     ch = b;
   }
-  const KeyT p = (ch == a) ? ka : (ch == b) ? kb : kc;
-  // ---- P1: ge/le flags ----
+  const uint32_t p = (ch == a) ? ka : (ch == b) ? kb : kc;
+  // ---- P1: ge/le flags (one bit per j in gem/lem), wave counts ----
   uint32_t gem = 0, lem = 0;
-  int cge = 0, cle = 0;
+  uint32_t kv[JM];
+#pragma unroll
+  for (int j = 0; j < JM; ++j) kv[j] = (uint32_t)key[min(pos0 + j * 64, hi - 1)];  // batched
 #pragma unroll
   for (int j = 0; j < JM; ++j) {
-    const int pos = wbeg + j * 64 + lane;
-    const bool valid = (j < J) && (pos < hi);
-    const KeyT kk = (pos == ch) ? klo : key[min(pos, hi - 1)];
-    const bool ge = valid && !(kk < p);
-    const bool le = valid && !(p < kk);
-    gem |= (uint32_t)ge << j;
-    lem |= (uint32_t)le << j;
-    cge += __popcll(__ballot(ge));
-    cle += __popcll(__ballot(le));
+    if (j >= J) break;
+    const int pos = pos0 + j * 64;
+    const bool inb = pos < hi;
+    const uint32_t kk = (pos == ch) ? klo : kv[j];
+    gem |= (inb && kk >= p) ? (1u << j) : 0u;
+    lem |= (inb && kk <= p) ? (1u << j) : 0u;
   }
+  // wave counts: per-lane popcounts, one packed 64-lane sum (row scans + 4 readlanes)
+  const int rs = row_scan16(__builtin_popcount(gem) | (__builtin_popcount(lem) << 16));
+  const int cnt = __builtin_amdgcn_readlane(rs, 15) + __builtin_amdgcn_readlane(rs, 31) +
+                  __builtin_amdgcn_readlane(rs, 47) + __builtin_amdgcn_readlane(rs, 63);
+  const int cge = cnt & 0xFFFF, cle = cnt >> 16;  // <= 1024 each
   int ge_before = 0, le_before = 0, tot_le = cle;
   if constexpr (NW > 1) {
-    if (lane == 0) {
-      sc.wa[wid] = cge;
-      sc.wb[wid] = cle;
-    }
+    static_assert(NW <= 16, "cross-wave scans use one 16-lane DPP row");
+    if (lane == 0) sc.wa[wid] = cge | (cle << 16);  // per-wave counts <= 1024: packed sums
     __syncthreads();  // B_a
-    tot_le = 0;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      const int x = sc.wa[w], y = sc.wb[w];
-      ge_before += (w < wid) ? x : 0;
-      le_before += (w < wid) ? y : 0;
-      tot_le += y;
-    }
+    const int scan = row_scan16(lane < NW ? sc.wa[lane] : 0);
+    const int before = wid ? __builtin_amdgcn_readlane(scan, wid - 1) : 0;
+    ge_before = before & 0xFFFF;
+    le_before = before >> 16;
+    tot_le = __builtin_amdgcn_readlane(scan, NW - 1) >> 16;
   }
   KVC_TICK(t1);
   // ---- P2: s rank table, swap count m, g_{m+1} (stores only) ----
-  if (tid == 0) {
-    kv_swap(key, idx, lo, ch);  // the median move, made physical
-    sc.m[par ^ 1] = 0;
-    sc.gnext[par ^ 1] = kBig;
-  }
+  if (tid == 0) kv_swap(key, idx, lo, ch);  // the median move, made physical
   int rge = ge_before, rle = le_before, nsw = 0, ff = kBig;
 #pragma unroll
   for (int j = 0; j < JM; ++j) {
+    if (j >= J) break;
     const bool ge = (gem >> j) & 1u, le = (lem >> j) & 1u;
-    const uint64_t bg = __ballot(ge), bl = __ballot(le);
-    const int A = rge + __popcll(bg & lt);
-    const int lin = rle + __popcll(bl & le_m);
-    const int pos = wbeg + j * 64 + lane;
-    if (le) spos[tot_le - lin + 1] = (uint16_t)pos;
+    const uint64_t bg = __builtin_amdgcn_ballot_w64(ge), bl = __builtin_amdgcn_ballot_w64(le);
+    const int A = mbcnt(bg, rge);                 // ge positions before this one
+    const int lin = mbcnt(bl, rle) + (le ? 1 : 0);  // le positions in [lo+1, pos]
     const bool cond = A + lin < tot_le;
-    nsw += (ge && cond) ? 1 : 0;               // per lane; reduced once below
-    ff = (ge && !cond) ? min(ff, pos) : ff;
+    const uint16_t pj = (uint16_t)(pos0 + j * 64);
+    spos[le ? tot_le - lin + 1 : kSposLen - 64 + lane] = pj;
+    gpos[(ge && cond) ? A + 1 : kGposLen - 64 + lane] = pj;  // swapped: rank A + 1 <= m
+    const uint64_t bc = __builtin_amdgcn_ballot_w64(cond);
+    nsw += __popcll(bg & bc);
+    const uint64_t bf = bg & ~bc;  // first unswapped ge: positions grow with j, so min = first
+    ff = min(ff, bf ? wbeg + j * 64 + (int)__builtin_ctzll(bf) : kBig);
     rge += __popcll(bg);
     rle += __popcll(bl);
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    nsw += __shfl_xor(nsw, o, 64);
-    ff = min(ff, __shfl_xor(ff, o, 64));
-  }
   int msw, gnext;
   if constexpr (NW > 1) {
-    if (lane == 0) {
-      if (nsw) atomicAdd(&sc.m[par], nsw);
-      if (ff != kBig) atomicMin(&sc.gnext[par], ff);
-    }
+    if (lane == 0) sc.wm[wid] = nsw | ((ff == kBig ? 0xFFFF : ff) << 16);  // positions < 2^14
     __syncthreads();  // B_b
-    msw = sc.m[par];
-    gnext = sc.gnext[par];
+    const uint32_t x = lane < NW ? (uint32_t)sc.wm[lane] : 0xFFFF0000u;
+    msw = __builtin_amdgcn_readlane(row_scan16((int)(x & 0xFFFFu)), NW - 1);
+    const uint64_t fb = __builtin_amdgcn_ballot_w64((x >> 16) != 0xFFFFu);  // waves in position order: first wins
+    gnext = fb ? (int)((uint32_t)__builtin_amdgcn_readlane((int)x, (int)__builtin_ctzll(fb)) >> 16)
+               : kBig;
   } else {
     wave_sync();
     msw = nsw;
     gnext = ff;
   }
   KVC_TICK(t2);
-  // ---- P4: the m swaps (disjoint pairs) in batches: spos loads, key/idx loads, stores ----
-  if (ge_before < msw) {
-    constexpr int JB = JM < 4 ? JM : 4;
-    rge = ge_before;
+  // ---- P4: the m swaps (disjoint pairs g_t <-> s_t), spread evenly over the NT lanes:
+  // rank-table loads, then key/idx loads, then stores ----
+  for (int base = 1; base <= msw; base += NT * 4) {
+    if (base + wid * 64 > msw) break;  // no rank left for this wave
+    int gp[4], sp[4];
 #pragma unroll
-    for (int j0 = 0; j0 < JM; j0 += JB) {
-      int sp[JB];
-      uint32_t act = 0;
+    for (int q = 0; q < 4; ++q) {
+      const int t = base + tid + q * NT;
+      gp[q] = gpos[t <= msw ? t : 0];
+      sp[q] = spos[t <= msw ? t : 0];
+    }
+    KeyT kg[4], ks[4];
+    uint16_t ig[4], is[4];
 #pragma unroll
-      for (int q = 0; q < JB; ++q) {
-        const bool ge = (gem >> (j0 + q)) & 1u;
-        const uint64_t bg = __ballot(ge);
-        const int t = rge + __popcll(bg & lt) + 1;
-        const bool doit = ge && t <= msw;
-        act |= (uint32_t)doit << q;
-        sp[q] = spos[doit ? t : 0];
-        rge += __popcll(bg);
-      }
-      KeyT kg[JB], ks[JB];
-      uint16_t ig[JB], is[JB];
+    for (int q = 0; q < 4; ++q) {
+      kg[q] = key[gp[q]];
+      ks[q] = key[sp[q]];
+      ig[q] = idx[gp[q]];
+      is[q] = idx[sp[q]];
+    }
 #pragma unroll
-      for (int q = 0; q < JB; ++q) {
-        const int pos = min(wbeg + (j0 + q) * 64 + lane, hi - 1);
-        kg[q] = key[pos];
-        ks[q] = key[sp[q]];
-        ig[q] = idx[pos];
-        is[q] = idx[sp[q]];
-      }
-#pragma unroll
-      for (int q = 0; q < JB; ++q) {
-        if ((act >> q) & 1u) {
-          const int pos = wbeg + (j0 + q) * 64 + lane;
-          key[pos] = ks[q];
-          key[sp[q]] = kg[q];
-          idx[pos] = is[q];
-          idx[sp[q]] = ig[q];
-        }
+    for (int q = 0; q < 4; ++q) {
+      if (base + tid + q * NT <= msw) {
+        key[gp[q]] = ks[q];
+        key[sp[q]] = kg[q];
+        idx[gp[q]] = is[q];
+        idx[sp[q]] = ig[q];
       }
     }
   }
@@ -484,9 +494,10 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
     acc[2] += t3 - t2;
     acc[3] += 1;
     acc[4] += (uint64_t)msw;
+    if (NT > 64) acc[25] = (t1 - t0) | ((t2 - t1) << 20) | ((t3 - t2) << 40);  // level split
   }
 #endif
-  return min(gnext, msw > 0 ? (int)spos[msw] : kBig);
+  return min(gnext, msw > 0 ? uni((int)spos[msw]) : kBig);
 }
 
 // The partition chain of libstdc++ introsort (topk = false) / introselect (topk = true),
@@ -530,19 +541,28 @@ __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, SelScalars<Ke
       return 0;
     }
     --depth;
-    const int par = level & 1;
     const int J = (hi - lo - 1 + NT - 1) / NT;
     int cut;
+#ifdef KVC_STAMPS
+    const uint64_t tl0 = __builtin_amdgcn_s_memtime();
+#endif
     if (J <= 1)
-      cut = partition_level<KeyT, NT, 1>(key, idx, spos, sc, lo, hi, par, acc);
+      cut = partition_level<KeyT, NT, 1>(key, idx, spos, sc, lo, hi, acc);
     else if (J <= 2)
-      cut = partition_level<KeyT, NT, 2>(key, idx, spos, sc, lo, hi, par, acc);
+      cut = partition_level<KeyT, NT, 2>(key, idx, spos, sc, lo, hi, acc);
     else if (J <= 4)
-      cut = partition_level<KeyT, NT, 4>(key, idx, spos, sc, lo, hi, par, acc);
+      cut = partition_level<KeyT, NT, 4>(key, idx, spos, sc, lo, hi, acc);
     else if (J <= 8)
-      cut = partition_level<KeyT, NT, 8>(key, idx, spos, sc, lo, hi, par, acc);
+      cut = partition_level<KeyT, NT, 8>(key, idx, spos, sc, lo, hi, acc);
     else
-      cut = partition_level<KeyT, NT, 16>(key, idx, spos, sc, lo, hi, par, acc);
+      cut = partition_level<KeyT, NT, 16>(key, idx, spos, sc, lo, hi, acc);
+#ifdef KVC_STAMPS
+    // per block level (first 8): cycles, and segment length  (slots 16.. of the row)
+    if (acc && NT > 64 && tid == 0 && level < 7) {
+      acc[11 + 2 * level] = __builtin_amdgcn_s_memtime() - tl0;
+      acc[12 + 2 * level] = acc[25];  // P1 | P2 << 20 | P4 << 40 of this level
+    }
+#endif
     if (topk) {  // std::__introselect: if (cut <= nth) first = cut; else last = cut;
       if (cut <= k - 1) lo = cut; else hi = cut;
     } else {     // std::__introsort_loop: recurse right, loop on the left part
@@ -627,10 +647,6 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
       }
     }
   }
-  if (tid == 0) {
-    sc.m[0] = 0;
-    sc.gnext[0] = kBig;
-  }
   __syncthreads();
   KVC_STAMP(1);
 
@@ -646,10 +662,10 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
     uint64_t* accw = nullptr;
 #ifdef KVC_STAMPS
     if (stamps) {
-      accb = stamps + blockIdx.x * 16 + 5;
-      accw = stamps + blockIdx.x * 16 + 10;
+      accb = stamps + blockIdx.x * 32 + 5;
+      accw = stamps + blockIdx.x * 32 + 10;
       if (tid == 0)
-        for (int q = 0; q < 10; ++q) accb[q] = 0;
+        for (int q = 0; q < 27; ++q) accb[q] = 0;
     }
 #endif
     const int st = run_chain<KeyT, kSelThreads>(key, idx, spos, sc, k, topk, thr, lo, hi, depth,
@@ -703,7 +719,7 @@ __global__ void __launch_bounds__(kSelThreads)
                   uint64_t* stamps) {
   typedef typename DTypeTraits<DT>::key_t KeyT;
   constexpr int ESZ = DTypeTraits<DT>::esz;
-  // LDS: key[kZoneMax] | idx[kZoneMax] (u16) | spos[kZoneMax + 8] (u16) | scalars
+  // LDS: key[kZoneMax] | idx[kZoneMax] (u16) | spos[kSposLen] | gpos[kGposLen] (u16) | scalars
   __shared__ __attribute__((aligned(16))) char smem[kSelLdsBytes<KeyT>];
   __shared__ SelScalars<KeyT> sc;
   const int row = blockIdx.x;
@@ -1069,7 +1085,7 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
     info->index_offset = off;
     off = round_up(off + (size_t)rows * info->index_row_stride * 4, 256);
 #ifdef KVC_STAMPS
-    off += (size_t)rows * 128;  // diagnostic stamp slots (16 x u64 per select row)
+    off += (size_t)rows * 256;  // diagnostic stamp slots (32 x u64 per select row)
 #endif
     info->workspace_bytes = off;
   }
@@ -1174,7 +1190,7 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
   if (wave_seg < 16) wave_seg = 16;
   if (wave_seg > 1024) wave_seg = 1024;
 #ifdef KVC_STAMPS
-  uint64_t* stamps = reinterpret_cast<uint64_t*>(w + info.workspace_bytes - info.rows * 128);
+  uint64_t* stamps = reinterpret_cast<uint64_t*>(w + info.workspace_bytes - info.rows * 256);
 #else
   uint64_t* stamps = nullptr;
 #endif

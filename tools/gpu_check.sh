@@ -31,6 +31,18 @@ if [ "$MODE" = "stamps" ]; then
   done
   cat gpurun_out/stamps.json
 fi
+if [ "$MODE" = "sqpmc" ]; then  # SQ counters of one kernel (regex $2) on the split path
+  cd /tmp && export TMPDIR=/tmp
+  i=0
+  for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS" \
+             "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES"; do
+    i=$((i+1))
+    timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex "${2:-select}" --output-format csv \
+        -d "$R/gpurun_out/sqpmc$i" -o run -- python3 "$R/tools/microbench.py" split 1 \
+        > "$R/gpurun_out/sqpmc$i.log" 2>&1 || exit $?
+  done
+  python3 "$R/tools/pmc_summary.py" "$R/gpurun_out/sqpmc1" "$R/gpurun_out/sqpmc2"
+fi
 if [ "$MODE" = "pmc" ]; then
   cd /tmp && export TMPDIR=/tmp
   for ctr in FETCH_SIZE WRITE_SIZE; do

@@ -40,7 +40,7 @@ for rep in range(3):
     assert rc == 0
     torch.cuda.synchronize()
 rows = int(info.rows)
-allst = ws[-rows * 128:].view(torch.int64).view(rows, 16).cpu().numpy().astype(np.float64)
+allst = ws[-rows * 256:].view(torch.int64).view(rows, 32).cpu().numpy().astype(np.float64)
 st = allst[:, :5]
 for nm, off in (("block", 5), ("wave", 10)):
     acc = allst[:, off:off + 5]
@@ -56,4 +56,10 @@ res["row_total_median"] = float(np.median(st[:, 4] - st[:, 0]))
 res["span_cycles"] = float(st[:, 4].max() - st[:, 0].min())
 starts = np.sort(st[:, 0] - st[:, 0].min())
 res["start_quantiles"] = [float(x) for x in np.percentile(starts, [0, 25, 50, 75, 100])]
+lv = allst[:, 16:32].reshape(rows, 8, 2)
+res["block_level_cycles_median"] = [float(np.median(lv[:, i, 0])) for i in range(7)]
+sp = allst[:, 16:32].reshape(rows, 8, 2)[:, :, 1].astype(np.int64)
+for q, nm in enumerate(("P1", "P2", "P4")):
+    res["block_level_" + nm + "_median"] = [float(np.median((sp[:, i] >> (20 * q)) & 0xFFFFF))
+                                            for i in range(7)]
 print(json.dumps(res))
