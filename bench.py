@@ -34,11 +34,14 @@ def algorithmic_bytes(es=2):
     return per_layer, score
 
 
-def pmc_traffic(kernel="kvc::score_kernel<1, 16>"):
+PMC_FILE = "profiles/r01_v6_pmc_traffic.json"  # tools/gpu_check.sh pmc + tools/pmc_traffic.py
+
+
+def pmc_traffic(kernel="kvc::score_kernel<1, 16, true>"):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC passes
-    (profiles/r01_v5_pmc_traffic.json: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) measured
-    on this exact workload; None if absent."""
-    path = os.path.join(ROOT, "profiles", "r01_v5_pmc_traffic.json")
+    (PMC_FILE: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) measured on this exact workload;
+    None if absent."""
+    path = os.path.join(ROOT, PMC_FILE)
     try:
         with open(path) as f:
             k = json.load(f)["kernels"][kernel]
@@ -175,7 +178,7 @@ def main():
                          "achieved": score_gbps, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                          "frac": score_gbps / PEAK_HBM_GBPS, "traffic": traffic,
                          "algorithmic_bytes_per_launch": score_bytes_layer * LAYERS,
-                         "traffic_source": "profiles/r01_v5_pmc_traffic.json (rocprofv3 --pmc)"},
+                         "traffic_source": PMC_FILE + " (rocprofv3 --pmc)"},
             "path_roofline": {"achieved": path_gbps, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                               "frac": path_gbps / PEAK_HBM_GBPS,
                               "bytes_per_layer": per_layer},

@@ -129,7 +129,7 @@ __device__ __forceinline__ void accum_chunk(float (&acc)[8], const uint4 x, int 
 // One 64-token tile of one (layer, b, h) row: coalesced 16-B loads -> per-wave LDS slab ->
 // one lane per token, torch.norm's 8-accumulator FMA order.  `wl` is this wave's slab
 // (kTile * ROWB bytes).  sc1 = publish the norms write-through for an in-launch consumer.
-template <int DT, int NC>
+template <int DT, int NC, bool NTL = false>
 __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int tt, int H,
                                            char* wl, char* norms, int64_t norm_stride,
                                            bool sc1) {
@@ -154,10 +154,18 @@ __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int t
     for (int it = 0; it < CP; ++it) {
       const int q = it * 64 + lane;
       const int tok = q / CP, c = q - (q / CP) * CP;
-      if (tok < ntok)
-        v[it] = *reinterpret_cast<const uint4*>(base + tok * sbytes + (ph * CP + c) * 16);
-      else
+      const char* src = base + tok * sbytes + (ph * CP + c) * 16;
+      if (tok < ntok) {
+        if constexpr (NTL) {
+          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+          const u32x4 w = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
+          v[it] = make_uint4(w.x, w.y, w.z, w.w);
+        } else {
+          v[it] = *reinterpret_cast<const uint4*>(src);
+        }
+      } else {
         v[it] = make_uint4(0, 0, 0, 0);
+      }
     }
 #pragma unroll
     for (int it = 0; it < CP; ++it) {
@@ -196,7 +204,7 @@ __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int t
   }
 }
 
-template <int DT, int NC>
+template <int DT, int NC, bool NTL>
 __global__ void __launch_bounds__(kScoreThreads)
     score_kernel(const kvc_layer_t* __restrict__ L, int nl, int H, int64_t total_tiles,
                  char* __restrict__ norms, int64_t norm_stride) {
@@ -218,7 +226,101 @@ __global__ void __launch_bounds__(kScoreThreads)
   const int tpr = (ly->zone_len + kTile - 1) / kTile;
   const int local = (int)(g - ly->tile0);
   const int row = local / tpr;
-  score_tile<DT, NC>(ly, row, local - row * tpr, H, lds[wid], norms, norm_stride, false);
+  score_tile<DT, NC, NTL>(ly, row, local - row * tpr, H, lds[wid], norms, norm_stride, false);
+}
+
+// SCORE, software-pipelined: each wave scores TPW consecutive tiles (any layers / rows) as a
+// sequence of TPW * NPH phase steps; the loads of step i + 1 are issued before step i is
+// transposed through LDS and reduced, so a wave keeps ~2 phases (2 x 8 KiB) in flight instead
+// of one.  (At one phase per wave the key stream is bound by bytes in flight per CU, not HBM.)
+template <int DT, int NC, int TPW>
+__global__ void __launch_bounds__(kScoreThreads)
+    score_pipe_kernel(const kvc_layer_t* __restrict__ L, int nl, int H, int64_t total_tiles,
+                      char* __restrict__ norms, int64_t norm_stride) {
+  constexpr int ESZ = DTypeTraits<DT>::esz;
+  constexpr int CP = (NC % 8 == 0) ? 8 : 10;
+  constexpr int NPH = NC / CP;
+  constexpr int ROWB = CP * 16 + 16;
+  constexpr int STEPS = TPW * NPH;
+  __shared__ __attribute__((aligned(16))) char lds[kScoreWaves][kTile * ROWB];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t g0 = ((int64_t)blockIdx.x * kScoreWaves + wid) * TPW;
+  if (g0 >= total_tiles) return;
+  const int nt = (int)min((int64_t)TPW, total_tiles - g0);
+  char* wl = lds[wid];
+  const char* tbase[TPW];  // per-tile source / destination (wave-uniform)
+  int64_t tsb[TPW];
+  int tnt[TPW];
+  char* tdst[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int64_t g = min(g0 + i, total_tiles - 1);
+    int lo = 0, hi = nl - 1;  // largest layer with tile0 <= g
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (L[mid].tile0 <= g) lo = mid; else hi = mid - 1;
+    }
+    const kvc_layer_t* ly = L + lo;
+    const int tpr = (ly->zone_len + kTile - 1) / kTile;
+    const int local = (int)(g - ly->tile0);
+    const int row = local / tpr, tt = local - row * tpr;
+    const int b = row / H, h = row - (row / H) * H;
+    const int tok0 = tt * kTile;
+    tnt[i] = min(kTile, ly->zone_len - tok0);
+    tsb[i] = ly->k_stride[2] * ESZ;
+    tbase[i] = static_cast<const char*>(ly->k) +
+               ((int64_t)b * ly->k_stride[0] + (int64_t)h * ly->k_stride[1] +
+                (int64_t)(ly->zone_start + tok0) * ly->k_stride[2]) * ESZ;
+    tdst[i] = norms + ((int64_t)(ly->row0 + row) * norm_stride + tok0) * ESZ;
+  }
+  uint4 buf[2][CP];
+  auto load = [&](int st) {
+    const int i = st / NPH, ph = st % NPH;
+#pragma unroll
+    for (int it = 0; it < CP; ++it) {
+      const int q = it * 64 + lane;
+      const int tok = q / CP, c = q - (q / CP) * CP;
+      buf[st & 1][it] = tok < tnt[i] ? *reinterpret_cast<const uint4*>(
+                                           tbase[i] + tok * tsb[i] + (ph * CP + c) * 16)
+                                     : make_uint4(0, 0, 0, 0);
+    }
+  };
+  load(0);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int st = 0; st < STEPS; ++st) {
+    const int i = st / NPH, ph = st % NPH;
+    if (i >= nt) break;
+    if (st + 1 < STEPS && (st + 1) / NPH < nt) load(st + 1);
+#pragma unroll
+    for (int it = 0; it < CP; ++it) {
+      const int q = it * 64 + lane;
+      const int tok = q / CP, c = q - (q / CP) * CP;
+      *reinterpret_cast<uint4*>(wl + tok * ROWB + c * 16) = buf[st & 1][it];
+    }
+    wave_sync();
+#pragma unroll
+    for (int c = 0; c < CP; ++c) {
+      const uint4 x = *reinterpret_cast<const uint4*>(wl + lane * ROWB + c * 16);
+      accum_chunk<DT, NC>(acc, x, ph * CP + c);
+    }
+    wave_sync();
+    if (ph == NPH - 1) {
+      if (lane < tnt[i]) {
+        float sum = acc[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) sum = sum + acc[j];
+        const float r = __builtin_sqrtf(sum);
+        if constexpr (DT == KVC_BF16)
+          reinterpret_cast<uint16_t*>(tdst[i])[lane] = (uint16_t)f32_to_bf16_rne(r);
+        else
+          reinterpret_cast<float*>(tdst[i])[lane] = r;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -730,7 +832,7 @@ __global__ void __launch_bounds__(kSelThreads)
 // ---------------------------------------------------------------------------------------------
 // GATHER
 // ---------------------------------------------------------------------------------------------
-template <int DT, int NC>
+template <int DT, int NC, bool NTS>
 __global__ void __launch_bounds__(kGatherThreads)
     gather_kernel(const kvc_layer_t* __restrict__ L, int H, int BH,
                   const int32_t* __restrict__ gidx, int64_t idx_stride) {
@@ -791,8 +893,16 @@ __global__ void __launch_bounds__(kGatherThreads)
           bq.z = canon_nan_bf16x2(bq.z); bq.w = canon_nan_bf16x2(bq.w);
         }
       }
-      *reinterpret_cast<uint4*>(ko + (int64_t)u * 16) = a;
-      *reinterpret_cast<uint4*>(vo + (int64_t)u * 16) = bq;
+      if constexpr (NTS) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(u32x4{a.x, a.y, a.z, a.w},
+                                    reinterpret_cast<u32x4*>(ko + (int64_t)u * 16));
+        __builtin_nontemporal_store(u32x4{bq.x, bq.y, bq.z, bq.w},
+                                    reinterpret_cast<u32x4*>(vo + (int64_t)u * 16));
+      } else {
+        *reinterpret_cast<uint4*>(ko + (int64_t)u * 16) = a;
+        *reinterpret_cast<uint4*>(vo + (int64_t)u * 16) = bq;
+      }
     }
   }
 }
@@ -944,7 +1054,7 @@ __global__ void __launch_bounds__(kSelThreads)
         const int tpr = (ly->zone_len + kTile - 1) / kTile;
         const int local = g - ly->tile0;
         const int row = local / tpr;
-        score_tile<DT, NC>(ly, row, local - row * tpr, H, wl, norms, norm_stride, true);
+        score_tile<DT, NC, true>(ly, row, local - row * tpr, H, wl, norms, norm_stride, true);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // norms reach L2 before the flags
       if (lane < ng)
@@ -1095,9 +1205,27 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
 template <int DT, int NC>
 static void launch_score(const kvc_layer_t* Ld, int nl, int H, int64_t tiles, char* norms,
                          int64_t nstride, hipStream_t s) {
+  int tpw = 1;  // tiles per wave; > 1 = the software-pipelined kernel (KVC_SCORE_TPW)
+  if (const char* e = getenv("KVC_SCORE_TPW")) tpw = atoi(e);
+  if (tpw == 2 || tpw == 4) {
+    const int64_t per = (int64_t)kScoreWaves * tpw;
+    const unsigned grid = (unsigned)((tiles + per - 1) / per);
+    if (tpw == 2)
+      hipLaunchKernelGGL((score_pipe_kernel<DT, NC, 2>), dim3(grid), dim3(kScoreThreads), 0, s,
+                         Ld, nl, H, tiles, norms, nstride);
+    else
+      hipLaunchKernelGGL((score_pipe_kernel<DT, NC, 4>), dim3(grid), dim3(kScoreThreads), 0, s,
+                         Ld, nl, H, tiles, norms, nstride);
+    return;
+  }
   const unsigned grid = (unsigned)((tiles + kScoreWaves - 1) / kScoreWaves);
-  hipLaunchKernelGGL((score_kernel<DT, NC>), dim3(grid), dim3(kScoreThreads), 0, s, Ld, nl, H,
-                     tiles, norms, nstride);
+  const char* ntl = getenv("KVC_SCORE_NT");  // keys are read once: non-temporal by default
+  if (!(ntl && strcmp(ntl, "0") == 0))
+    hipLaunchKernelGGL((score_kernel<DT, NC, true>), dim3(grid), dim3(kScoreThreads), 0, s, Ld,
+                       nl, H, tiles, norms, nstride);
+  else
+    hipLaunchKernelGGL((score_kernel<DT, NC, false>), dim3(grid), dim3(kScoreThreads), 0, s, Ld,
+                       nl, H, tiles, norms, nstride);
 }
 
 // `work` = max n_out over layers; grid = (rows, token blocks)
@@ -1105,7 +1233,12 @@ template <int DT, int NC>
 static void launch_gather(const kvc_layer_t* Ld, int nl, int H, int BH, const int32_t* idx,
                           int64_t istride, int64_t work, hipStream_t s) {
   const dim3 grid((unsigned)(nl * BH), (unsigned)((work + kGatherTokens - 1) / kGatherTokens));
-  hipLaunchKernelGGL((gather_kernel<DT, NC>), grid, dim3(kGatherThreads), 0, s, Ld, H, BH, idx,
+const char* nts = getenv("KVC_GATHER_NT");  // outputs are written once: non-temporal default
+  if (!(nts && strcmp(nts, "0") == 0))
+      hipLaunchKernelGGL((gather_kernel<DT, NC, true>), grid, dim3(kGatherThreads), 0, s, Ld, H, BH, idx,
+                     istride);
+  else
+      hipLaunchKernelGGL((gather_kernel<DT, NC, false>), grid, dim3(kGatherThreads), 0, s, Ld, H, BH, idx,
                      istride);
 }
 
@@ -1195,11 +1328,13 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
   uint64_t* stamps = nullptr;
 #endif
   (void)hipGetLastError();
-  // Fused persistent path: all phases, no caller-provided indices, 128/256-byte rows (wider
-  // rows need more than the 128 VGPRs a 1024-thread workgroup allows).  KVC_FUSED=0 forces the
-  // three-kernel path (A/B comparisons, tests).
+  // Fused persistent path (opt-in, KVC_FUSED=1): all phases, no caller-provided indices,
+  // 128/256-byte rows (wider rows need more than the 128 VGPRs a 1024-thread workgroup allows).
+  // It overlaps selection with the key stream, but on the headline workload the three-kernel
+  // path with non-temporal streams is faster, so that is the default.
   bool fused = p->phases == KVC_PHASE_ALL && !p->external_index && (nc == 8 || nc == 16);
-  if (const char* e = getenv("KVC_FUSED")) fused = fused && strcmp(e, "0") != 0;
+  const char* fe = getenv("KVC_FUSED");
+  fused = fused && fe && strcmp(fe, "1") == 0;
   if (fused) {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||

@@ -13,7 +13,8 @@ from kvcompress.methods import fix_size_l2_compress  # noqa: E402
 
 # variant = split | unfused | fused[@W]:  split = three kernels timed per phase; unfused = three
 # kernels timed as one launch (KVC_FUSED=0); fused = the persistent kernel (one launch), @W =
-# W workgroups start on the row queue (KVC_SEL_WGS)
+# W workgroups start on the row queue (KVC_SEL_WGS); suffix %T = T score tiles per wave
+# (KVC_SCORE_TPW, software-pipelined score kernel)
 variants = sys.argv[1].split(",") if len(sys.argv) > 1 else ["split", "unfused", "fused"]
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 dev = torch.device("cuda:0")
@@ -25,7 +26,12 @@ res = {v: {} for v in variants}
 ref = None
 for r in range(rounds):
     for v in variants:
-        name, _, diag = v.partition("#")
+        v1, _, ntl = v.partition("!")  # !s / !g: temporal score loads / gather stores
+        os.environ["KVC_SCORE_NT"] = "0" if "s" in ntl else "1"
+        os.environ["KVC_GATHER_NT"] = "0" if "g" in ntl else "1"
+        v0, _, tpw = v1.partition("%")
+        os.environ["KVC_SCORE_TPW"] = tpw or "1"
+        name, _, diag = v0.partition("#")
         name, _, wgs = name.partition("@")
         os.environ["KVC_FUSED_DIAG"] = diag or "0"
         os.environ["KVC_FUSED"] = "1" if name == "fused" else "0"
@@ -33,7 +39,7 @@ for r in range(rounds):
             os.environ["KVC_SEL_WGS"] = wgs
         else:
             os.environ.pop("KVC_SEL_WGS", None)
-        t = _engine.PhaseTimer(split=(v == "split"))
+        t = _engine.PhaseTimer(split=(name == "split"))
         _engine.set_phase_timer(t)
         torch.cuda.synchronize()
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
