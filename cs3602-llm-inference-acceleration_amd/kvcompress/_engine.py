@@ -88,6 +88,8 @@ def _check_tensors(j: Segments):
 def _prep(t):
     """Last dim contiguous and 16-byte aligned rows (else a device-side contiguous copy)."""
     es = t.element_size()
+    if t.is_contiguous() and t.data_ptr() % 16 == 0 and (t.size(3) * es) % 16 == 0:
+        return t  # the common case, one C call
     ok = (t.stride(3) == 1 and t.data_ptr() % 16 == 0 and
           all((t.stride(d) * es) % 16 == 0 or t.size(d) == 1 for d in range(3)))
     return t if ok else t.contiguous()
@@ -151,24 +153,27 @@ def _run_group(device, dtype, B, H, D, js, out_list, order, algo):
     if external and not all(j.ext_index is not None or j.n_select == 0 for j in js):
         raise RuntimeError("mixed external / engine-selected layers in one group")
     table = np.zeros(n, dtype=N.LAYER_DTYPE)
-    keep = []  # prepared (possibly contiguous-copied) inputs stay alive until enqueued
-    outs = []
-    for i, j in enumerate(js):
-        k, v = _prep(j.keys), _prep(j.values)
-        keep.append((k, v))
-        n_out = j.sink_len + j.n_select + j.tail_len
-        ko = torch.empty((B, H, n_out, D), dtype=dtype, device=device)
-        vo = torch.empty((B, H, n_out, D), dtype=dtype, device=device)
-        outs.append((ko, vo))
-        t = table[i]
-        t["k"], t["v"] = k.data_ptr(), v.data_ptr()
-        t["k_out"], t["v_out"] = ko.data_ptr(), vo.data_ptr()
-        t["k_stride"] = k.stride()[:3]
-        t["v_stride"] = v.stride()[:3]
-        t["seq_len"] = k.shape[2]
-        t["zone_start"], t["zone_len"], t["n_select"] = j.zone_start, j.zone_len, j.n_select
-        t["sink_len"], t["tail_start"], t["tail_len"] = j.sink_len, j.tail_start, j.tail_len
-        t["pool_kernel"], t["score_mode"] = j.pool_kernel, j.score_mode
+    ks = [_prep(j.keys) for j in js]  # prepared inputs stay alive until enqueued
+    vs = [_prep(j.values) for j in js]
+    n_outs = [j.sink_len + j.n_select + j.tail_len for j in js]
+    if all(x == n_outs[0] for x in n_outs):
+        # one allocation for every output of the call (decode steps: 64 tensors per token);
+        # each layer's K / V is a disjoint contiguous view of it
+        o = torch.empty((2 * n, B, H, n_outs[0], D), dtype=dtype, device=device).unbind(0)
+        kos, vos = o[:n], o[n:]
+    else:
+        kos = [torch.empty((B, H, x, D), dtype=dtype, device=device) for x in n_outs]
+        vos = [torch.empty((B, H, x, D), dtype=dtype, device=device) for x in n_outs]
+    table["k"] = [t.data_ptr() for t in ks]
+    table["v"] = [t.data_ptr() for t in vs]
+    table["k_out"] = [t.data_ptr() for t in kos]
+    table["v_out"] = [t.data_ptr() for t in vos]
+    table["k_stride"] = [t.stride()[:3] for t in ks]
+    table["v_stride"] = [t.stride()[:3] for t in vs]
+    table["seq_len"] = [t.shape[2] for t in ks]
+    for f in ("zone_start", "zone_len", "n_select", "sink_len", "tail_start", "tail_len",
+              "pool_kernel", "score_mode"):
+        table[f] = [getattr(j, f) for j in js]
 
     def params():
         return N.Params(dtype=_SUPPORTED[dtype], batch=B, heads=H, head_dim=D, order=order,
@@ -184,5 +189,5 @@ def _run_group(device, dtype, B, H, D, js, out_list, order, algo):
         _launch(p, table, ws, info, torch.cuda.current_stream(device), p.phases)
         if _timer is not None and _timer.workspaces is not None:
             _timer.workspaces.append((ws, info))
-    for j, (ko, vo) in zip(js, outs):
+    for j, ko, vo in zip(js, kos, vos):
         out_list[j.layer_idx] = (ko, vo)
