@@ -34,7 +34,7 @@ def algorithmic_bytes(es=2):
     return per_layer, score
 
 
-PMC_FILE = "profiles/r01_v6_pmc_traffic.json"  # tools/gpu_check.sh pmc + tools/pmc_traffic.py
+PMC_FILE = "profiles/r01_v7_pmc_traffic.json"  # tools/gpu_check.sh pmc + tools/pmc_traffic.py
 
 
 def pmc_traffic(kernel="kvc::score_kernel<1, 16, true>"):

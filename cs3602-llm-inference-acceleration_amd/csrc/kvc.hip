@@ -36,6 +36,13 @@ constexpr int kWaveSeg = 128;    // default: segments this short are finished by
 constexpr int kGatherThreads = 256;
 constexpr int kGatherTokens = 64;  // output tokens per gather block
 constexpr int kBig = 0x7FFFFFFF;
+// Layer tables travel to the score / select / gather kernels BY VALUE in the kernel arguments
+// (chunks of kArgLayers, 8.7 KiB): no host->device table copy, whose completion would stand
+// ~10 us between the copy and the first kernel of every call.
+constexpr int kArgLayers = 64;
+struct LayerChunk {
+  kvc_layer_t l[kArgLayers];
+};
 
 template <int DT>
 struct DTypeTraits;
@@ -206,14 +213,16 @@ __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int t
 
 template <int DT, int NC, bool NTL>
 __global__ void __launch_bounds__(kScoreThreads)
-    score_kernel(const kvc_layer_t* __restrict__ L, int nl, int H, int64_t total_tiles,
+    score_kernel(const LayerChunk T, int nl, int H, int64_t tile_base, int64_t chunk_tiles,
                  char* __restrict__ norms, int64_t norm_stride) {
   constexpr int CP = (NC % 8 == 0) ? 8 : 10;
   constexpr int ROWB = CP * 16 + 16;
   __shared__ __attribute__((aligned(16))) char lds[kScoreWaves][kTile * ROWB];
+  const kvc_layer_t* L = T.l;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t g = (int64_t)blockIdx.x * kScoreWaves + wid;
-  if (g >= total_tiles) return;
+  const int64_t gl = (int64_t)blockIdx.x * kScoreWaves + wid;
+  if (gl >= chunk_tiles) return;
+  const int64_t g = tile_base + gl;  // global tile index (kvc_plan's tile0 numbering)
   int lo = 0, hi = nl - 1;  // largest layer with tile0 <= g
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -227,100 +236,6 @@ __global__ void __launch_bounds__(kScoreThreads)
   const int local = (int)(g - ly->tile0);
   const int row = local / tpr;
   score_tile<DT, NC, NTL>(ly, row, local - row * tpr, H, lds[wid], norms, norm_stride, false);
-}
-
-// SCORE, software-pipelined: each wave scores TPW consecutive tiles (any layers / rows) as a
-// sequence of TPW * NPH phase steps; the loads of step i + 1 are issued before step i is
-// transposed through LDS and reduced, so a wave keeps ~2 phases (2 x 8 KiB) in flight instead
-// of one.  (At one phase per wave the key stream is bound by bytes in flight per CU, not HBM.)
-template <int DT, int NC, int TPW>
-__global__ void __launch_bounds__(kScoreThreads)
-    score_pipe_kernel(const kvc_layer_t* __restrict__ L, int nl, int H, int64_t total_tiles,
-                      char* __restrict__ norms, int64_t norm_stride) {
-  constexpr int ESZ = DTypeTraits<DT>::esz;
-  constexpr int CP = (NC % 8 == 0) ? 8 : 10;
-  constexpr int NPH = NC / CP;
-  constexpr int ROWB = CP * 16 + 16;
-  constexpr int STEPS = TPW * NPH;
-  __shared__ __attribute__((aligned(16))) char lds[kScoreWaves][kTile * ROWB];
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t g0 = ((int64_t)blockIdx.x * kScoreWaves + wid) * TPW;
-  if (g0 >= total_tiles) return;
-  const int nt = (int)min((int64_t)TPW, total_tiles - g0);
-  char* wl = lds[wid];
-  const char* tbase[TPW];  // per-tile source / destination (wave-uniform)
-  int64_t tsb[TPW];
-  int tnt[TPW];
-  char* tdst[TPW];
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    const int64_t g = min(g0 + i, total_tiles - 1);
-    int lo = 0, hi = nl - 1;  // largest layer with tile0 <= g
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (L[mid].tile0 <= g) lo = mid; else hi = mid - 1;
-    }
-    const kvc_layer_t* ly = L + lo;
-    const int tpr = (ly->zone_len + kTile - 1) / kTile;
-    const int local = (int)(g - ly->tile0);
-    const int row = local / tpr, tt = local - row * tpr;
-    const int b = row / H, h = row - (row / H) * H;
-    const int tok0 = tt * kTile;
-    tnt[i] = min(kTile, ly->zone_len - tok0);
-    tsb[i] = ly->k_stride[2] * ESZ;
-    tbase[i] = static_cast<const char*>(ly->k) +
-               ((int64_t)b * ly->k_stride[0] + (int64_t)h * ly->k_stride[1] +
-                (int64_t)(ly->zone_start + tok0) * ly->k_stride[2]) * ESZ;
-    tdst[i] = norms + ((int64_t)(ly->row0 + row) * norm_stride + tok0) * ESZ;
-  }
-  uint4 buf[2][CP];
-  auto load = [&](int st) {
-    const int i = st / NPH, ph = st % NPH;
-#pragma unroll
-    for (int it = 0; it < CP; ++it) {
-      const int q = it * 64 + lane;
-      const int tok = q / CP, c = q - (q / CP) * CP;
-      buf[st & 1][it] = tok < tnt[i] ? *reinterpret_cast<const uint4*>(
-                                           tbase[i] + tok * tsb[i] + (ph * CP + c) * 16)
-                                     : make_uint4(0, 0, 0, 0);
-    }
-  };
-  load(0);
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int st = 0; st < STEPS; ++st) {
-    const int i = st / NPH, ph = st % NPH;
-    if (i >= nt) break;
-    if (st + 1 < STEPS && (st + 1) / NPH < nt) load(st + 1);
-#pragma unroll
-    for (int it = 0; it < CP; ++it) {
-      const int q = it * 64 + lane;
-      const int tok = q / CP, c = q - (q / CP) * CP;
-      *reinterpret_cast<uint4*>(wl + tok * ROWB + c * 16) = buf[st & 1][it];
-    }
-    wave_sync();
-#pragma unroll
-    for (int c = 0; c < CP; ++c) {
-      const uint4 x = *reinterpret_cast<const uint4*>(wl + lane * ROWB + c * 16);
-      accum_chunk<DT, NC>(acc, x, ph * CP + c);
-    }
-    wave_sync();
-    if (ph == NPH - 1) {
-      if (lane < tnt[i]) {
-        float sum = acc[0];
-#pragma unroll
-        for (int j = 1; j < 8; ++j) sum = sum + acc[j];
-        const float r = __builtin_sqrtf(sum);
-        if constexpr (DT == KVC_BF16)
-          reinterpret_cast<uint16_t*>(tdst[i])[lane] = (uint16_t)f32_to_bf16_rne(r);
-        else
-          reinterpret_cast<float*>(tdst[i])[lane] = r;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-    }
-  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -815,7 +730,7 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
 
 template <int DT>
 __global__ void __launch_bounds__(kSelThreads)
-    select_kernel(const kvc_layer_t* __restrict__ L, int BH, int order, int algo,
+    select_kernel(const LayerChunk T, int BH, int order, int algo,
                   const char* __restrict__ norms, int64_t norm_stride,
                   int32_t* __restrict__ out_idx, int64_t idx_stride, int wave_seg,
                   uint64_t* stamps) {
@@ -824,9 +739,11 @@ __global__ void __launch_bounds__(kSelThreads)
   // LDS: key[kZoneMax] | idx[kZoneMax] (u16) | spos[kSposLen] | gpos[kGposLen] (u16) | scalars
   __shared__ __attribute__((aligned(16))) char smem[kSelLdsBytes<KeyT>];
   __shared__ SelScalars<KeyT> sc;
-  const int row = blockIdx.x;
-  select_body<DT, false>(L + row / BH, order, algo, norms + (int64_t)row * norm_stride * ESZ,
-                  out_idx + (int64_t)row * idx_stride, nullptr, smem, sc, wave_seg, stamps);
+  const kvc_layer_t* ly = T.l + blockIdx.x / BH;
+  const int row = ly->row0 + (int)(blockIdx.x % BH);  // global workspace row
+  select_body<DT, false>(ly, order, algo, norms + (int64_t)row * norm_stride * ESZ,
+                         out_idx + (int64_t)row * idx_stride, nullptr, smem, sc, wave_seg,
+                         stamps);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -834,8 +751,9 @@ __global__ void __launch_bounds__(kSelThreads)
 // ---------------------------------------------------------------------------------------------
 template <int DT, int NC, bool NTS>
 __global__ void __launch_bounds__(kGatherThreads)
-    gather_kernel(const kvc_layer_t* __restrict__ L, int H, int BH,
+    gather_kernel(const LayerChunk T, int H, int BH,
                   const int32_t* __restrict__ gidx, int64_t idx_stride) {
+  const kvc_layer_t* L = T.l;
   // grid = (rows, output-token blocks); one block copies kGatherTokens output rows of K and V
   constexpr int ESZ = DTypeTraits<DT>::esz;
   constexpr int ITERS = (kGatherTokens * NC + kGatherThreads - 1) / kGatherThreads;
@@ -1203,55 +1121,42 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
 }
 
 template <int DT, int NC>
-static void launch_score(const kvc_layer_t* Ld, int nl, int H, int64_t tiles, char* norms,
-                         int64_t nstride, hipStream_t s) {
-  int tpw = 1;  // tiles per wave; > 1 = the software-pipelined kernel (KVC_SCORE_TPW)
-  if (const char* e = getenv("KVC_SCORE_TPW")) tpw = atoi(e);
-  if (tpw == 2 || tpw == 4) {
-    const int64_t per = (int64_t)kScoreWaves * tpw;
-    const unsigned grid = (unsigned)((tiles + per - 1) / per);
-    if (tpw == 2)
-      hipLaunchKernelGGL((score_pipe_kernel<DT, NC, 2>), dim3(grid), dim3(kScoreThreads), 0, s,
-                         Ld, nl, H, tiles, norms, nstride);
-    else
-      hipLaunchKernelGGL((score_pipe_kernel<DT, NC, 4>), dim3(grid), dim3(kScoreThreads), 0, s,
-                         Ld, nl, H, tiles, norms, nstride);
-    return;
-  }
-  const unsigned grid = (unsigned)((tiles + kScoreWaves - 1) / kScoreWaves);
+static void launch_score(const LayerChunk& T, int nl, int H, int64_t tile_base,
+                         int64_t chunk_tiles, char* norms, int64_t nstride, hipStream_t s) {
+  const unsigned grid = (unsigned)((chunk_tiles + kScoreWaves - 1) / kScoreWaves);
   const char* ntl = getenv("KVC_SCORE_NT");  // keys are read once: non-temporal by default
   if (!(ntl && strcmp(ntl, "0") == 0))
-    hipLaunchKernelGGL((score_kernel<DT, NC, true>), dim3(grid), dim3(kScoreThreads), 0, s, Ld,
-                       nl, H, tiles, norms, nstride);
+    hipLaunchKernelGGL((score_kernel<DT, NC, true>), dim3(grid), dim3(kScoreThreads), 0, s, T,
+                       nl, H, tile_base, chunk_tiles, norms, nstride);
   else
-    hipLaunchKernelGGL((score_kernel<DT, NC, false>), dim3(grid), dim3(kScoreThreads), 0, s, Ld,
-                       nl, H, tiles, norms, nstride);
+    hipLaunchKernelGGL((score_kernel<DT, NC, false>), dim3(grid), dim3(kScoreThreads), 0, s, T,
+                       nl, H, tile_base, chunk_tiles, norms, nstride);
 }
 
-// `work` = max n_out over layers; grid = (rows, token blocks)
+// `work` = max n_out over the chunk's layers; grid = (rows, token blocks)
 template <int DT, int NC>
-static void launch_gather(const kvc_layer_t* Ld, int nl, int H, int BH, const int32_t* idx,
+static void launch_gather(const LayerChunk& T, int nl, int H, int BH, const int32_t* idx,
                           int64_t istride, int64_t work, hipStream_t s) {
   const dim3 grid((unsigned)(nl * BH), (unsigned)((work + kGatherTokens - 1) / kGatherTokens));
-const char* nts = getenv("KVC_GATHER_NT");  // outputs are written once: non-temporal default
+  const char* nts = getenv("KVC_GATHER_NT");  // outputs are written once: non-temporal default
   if (!(nts && strcmp(nts, "0") == 0))
-      hipLaunchKernelGGL((gather_kernel<DT, NC, true>), grid, dim3(kGatherThreads), 0, s, Ld, H, BH, idx,
-                     istride);
+    hipLaunchKernelGGL((gather_kernel<DT, NC, true>), grid, dim3(kGatherThreads), 0, s, T, H, BH,
+                       idx, istride);
   else
-      hipLaunchKernelGGL((gather_kernel<DT, NC, false>), grid, dim3(kGatherThreads), 0, s, Ld, H, BH, idx,
-                     istride);
+    hipLaunchKernelGGL((gather_kernel<DT, NC, false>), grid, dim3(kGatherThreads), 0, s, T, H,
+                       BH, idx, istride);
 }
 
 template <int DT>
-static void dispatch_nc(int nc, bool score, const kvc_layer_t* Ld, int nl, int H, int BH,
-                        int64_t work, char* norms, int64_t nstride, const int32_t* idx,
-                        int64_t istride, hipStream_t s) {
+static void dispatch_nc(int nc, bool score, const LayerChunk& T, int nl, int H, int BH,
+                        int64_t base, int64_t work, char* norms, int64_t nstride,
+                        const int32_t* idx, int64_t istride, hipStream_t s) {
 #define KVC_NC_CASE(NCV)                                                   \
   case NCV:                                                                \
     if (score)                                                             \
-      launch_score<DT, NCV>(Ld, nl, H, work, norms, nstride, s);           \
+      launch_score<DT, NCV>(T, nl, H, base, work, norms, nstride, s);      \
     else                                                                   \
-      launch_gather<DT, NCV>(Ld, nl, H, BH, idx, istride, work, s);        \
+      launch_gather<DT, NCV>(T, nl, H, BH, idx, istride, work, s);         \
     break;
   switch (nc) {
     KVC_NC_CASE(8)
@@ -1302,20 +1207,12 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
   if (!ws || ws_bytes < info.workspace_bytes) return KVC_E_WORKSPACE;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   char* w = static_cast<char*>(ws);
-  if (!layers_dev) {
-    if (hipMemcpyAsync(w + info.desc_offset, layers, (size_t)nl * sizeof(kvc_layer_t),
-                       hipMemcpyHostToDevice, s) != hipSuccess)
-      return KVC_E_HIP;
-    layers_dev = reinterpret_cast<const kvc_layer_t*>(w + info.desc_offset);
-  }
   const int es = esize(p->dtype);
   const int nc = p->head_dim * es / 16;
   const int H = p->heads;
   const int BH = p->batch * p->heads;
   char* norms = w + info.norm_offset;
   int32_t* idx = reinterpret_cast<int32_t*>(w + info.index_offset);
-  bool any_sel = false;
-  for (int l = 0; l < nl; ++l) any_sel |= layers[l].n_select > 0;
   // wave hand-off threshold (<= 1024: the wave chain covers 64 lanes x 16 positions);
   // KVC_WAVE_SEG overrides it for tuning sweeps
   int wave_seg = kWaveSeg;
@@ -1336,6 +1233,12 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
   const char* fe = getenv("KVC_FUSED");
   fused = fused && fe && strcmp(fe, "1") == 0;
   if (fused) {
+    if (!layers_dev) {  // the persistent kernel reads the whole table from device memory
+      if (hipMemcpyAsync(w + info.desc_offset, layers, (size_t)nl * sizeof(kvc_layer_t),
+                         hipMemcpyHostToDevice, s) != hipSuccess)
+        return KVC_E_HIP;
+      layers_dev = reinterpret_cast<const kvc_layer_t*>(w + info.desc_offset);
+    }
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -1370,32 +1273,45 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
 #undef KVC_FUSED_LAUNCH
     return hipGetLastError() == hipSuccess ? KVC_OK : KVC_E_HIP;
   }
-  if ((p->phases & KVC_PHASE_SCORE) && info.score_tiles > 0 && !p->external_index) {
-    if (p->dtype == KVC_BF16)
-      dispatch_nc<KVC_BF16>(nc, true, layers_dev, nl, H, BH, info.score_tiles, norms,
-                            info.norm_row_stride, idx, info.index_row_stride, s);
-    else
-      dispatch_nc<KVC_F32>(nc, true, layers_dev, nl, H, BH, info.score_tiles, norms,
-                           info.norm_row_stride, idx, info.index_row_stride, s);
-  }
-  if ((p->phases & KVC_PHASE_SELECT) && any_sel && !p->external_index) {
-    const dim3 grid((unsigned)info.rows), block(kSelThreads);
-    if (p->dtype == KVC_BF16)
-      hipLaunchKernelGGL(select_kernel<KVC_BF16>, grid, block, 0, s, layers_dev, BH, p->order,
-                         p->algo, norms, info.norm_row_stride, idx, info.index_row_stride, wave_seg, stamps);
-    else
-      hipLaunchKernelGGL(select_kernel<KVC_F32>, grid, block, 0, s, layers_dev, BH, p->order,
-                         p->algo, norms, info.norm_row_stride, idx, info.index_row_stride, wave_seg, stamps);
-  }
-  if ((p->phases & KVC_PHASE_GATHER) && info.gather_units > 0) {
+  // Three kernels per chunk of <= kArgLayers layers, each with the chunk's table by value.
+  for (int c0 = 0; c0 < nl; c0 += kArgLayers) {
+    const int cn = nl - c0 < kArgLayers ? nl - c0 : kArgLayers;
+    LayerChunk T;
+    memcpy(T.l, layers + c0, (size_t)cn * sizeof(kvc_layer_t));
+    const int64_t tile_base = layers[c0].tile0;
+    const int64_t tile_end = c0 + cn < nl ? (int64_t)layers[c0 + cn].tile0 : info.score_tiles;
+    bool sel = false;
     int64_t max_out = 0;
-    for (int l = 0; l < nl; ++l) max_out = layers[l].n_out > max_out ? layers[l].n_out : max_out;
-    if (p->dtype == KVC_BF16)
-      dispatch_nc<KVC_BF16>(nc, false, layers_dev, nl, H, BH, max_out, norms,
-                            info.norm_row_stride, idx, info.index_row_stride, s);
-    else
-      dispatch_nc<KVC_F32>(nc, false, layers_dev, nl, H, BH, max_out, norms,
-                           info.norm_row_stride, idx, info.index_row_stride, s);
+    for (int l = c0; l < c0 + cn; ++l) {
+      sel |= layers[l].n_select > 0;
+      max_out = layers[l].n_out > max_out ? layers[l].n_out : max_out;
+    }
+    if ((p->phases & KVC_PHASE_SCORE) && tile_end > tile_base && !p->external_index) {
+      if (p->dtype == KVC_BF16)
+        dispatch_nc<KVC_BF16>(nc, true, T, cn, H, BH, tile_base, tile_end - tile_base, norms,
+                              info.norm_row_stride, idx, info.index_row_stride, s);
+      else
+        dispatch_nc<KVC_F32>(nc, true, T, cn, H, BH, tile_base, tile_end - tile_base, norms,
+                             info.norm_row_stride, idx, info.index_row_stride, s);
+    }
+    if ((p->phases & KVC_PHASE_SELECT) && sel && !p->external_index) {
+      const dim3 grid((unsigned)(cn * BH)), block(kSelThreads);
+      uint64_t* st = stamps ? stamps + (size_t)layers[c0].row0 * 32 : nullptr;
+      if (p->dtype == KVC_BF16)
+        hipLaunchKernelGGL(select_kernel<KVC_BF16>, grid, block, 0, s, T, BH, p->order, p->algo,
+                           norms, info.norm_row_stride, idx, info.index_row_stride, wave_seg, st);
+      else
+        hipLaunchKernelGGL(select_kernel<KVC_F32>, grid, block, 0, s, T, BH, p->order, p->algo,
+                           norms, info.norm_row_stride, idx, info.index_row_stride, wave_seg, st);
+    }
+    if ((p->phases & KVC_PHASE_GATHER) && max_out > 0) {
+      if (p->dtype == KVC_BF16)
+        dispatch_nc<KVC_BF16>(nc, false, T, cn, H, BH, 0, max_out, norms, info.norm_row_stride,
+                              idx, info.index_row_stride, s);
+      else
+        dispatch_nc<KVC_F32>(nc, false, T, cn, H, BH, 0, max_out, norms, info.norm_row_stride,
+                             idx, info.index_row_stride, s);
+    }
   }
   return hipGetLastError() == hipSuccess ? KVC_OK : KVC_E_HIP;
 }

@@ -108,12 +108,12 @@ def execute(jobs: List[Segments], out_list: list, order: int, algo: int):
 
 
 def _upload(params, table, device, js, B, H):
-    """Plan one table, allocate its workspace and enqueue the descriptor upload (current stream)."""
+    """Plan one table and allocate its workspace.  The table itself travels in the kernels'
+    arguments (the library copies it to the workspace only for the opt-in fused kernel);
+    caller-provided indices (strategy="random") are copied into the index region here."""
     rc, info = N.plan(params, table)
     N.check(rc, "kvc_plan")
     ws = torch.empty(max(int(info.workspace_bytes), 256), dtype=torch.uint8, device=device)
-    tbl = torch.from_numpy(table.view(np.uint8)).pin_memory()
-    ws[info.desc_offset:info.desc_offset + tbl.numel()].copy_(tbl, non_blocking=True)
     if params.external_index:
         istride = int(info.index_row_stride)
         iv = ws[info.index_offset:info.index_offset + int(info.rows) * istride * 4]
@@ -126,7 +126,7 @@ def _upload(params, table, device, js, B, H):
 
 
 def _launch(params, table, ws, info, stream, phases):
-    dev_tbl = ws.data_ptr() + int(info.desc_offset)
+    dev_tbl = 0  # NULL: by-value tables (the library uploads one itself if it needs it)
     saved = params.phases
     steps = ((("score", N.PHASE_SCORE), ("select", N.PHASE_SELECT), ("gather", N.PHASE_GATHER))
              if _timer is not None and _timer.split else (("all", phases),))

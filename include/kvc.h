@@ -21,8 +21,8 @@
  * -> cat); the engine reproduces their results bit-exactly, including libstdc++'s introsort /
  * introselect tie order, torch.norm's 8-lane FMA order, and torch.gather's bf16 NaN rewrite.
  *
- * Phases (stream-ordered on `stream`; for KVC_PHASE_ALL with 8/16/32 16-byte chunks per row
- * they run as ONE persistent kernel that overlaps selection with key streaming):
+ * Phases (stream-ordered on `stream`, one kernel each per chunk of <= 64 layers; KVC_FUSED=1
+ * runs KVC_PHASE_ALL on 128/256-byte rows as one persistent kernel instead):
  *   SCORE  : key L2 norms of every zone token           -> workspace norm region
  *   SELECT : per (layer,b,h) row: snapkv scoring (opt.), reference-exact k-selection,
  *            ascending zone-local indices                -> workspace index region (int32)
@@ -133,10 +133,11 @@ const char* kvc_status_string(int status);
 int kvc_plan(const kvc_params_t* params, kvc_layer_t* layers, int num_layers,
              kvc_plan_info_t* info);
 
-/* Launches the requested phases.  `layers` is the host table filled by kvc_plan();
- * `layers_dev` is a device copy of it (e.g. at workspace + info.desc_offset) that the caller
- * has already made stream-ordered with this launch.  Passing layers_dev = NULL makes the library
- * enqueue that copy itself (hipMemcpyAsync from `layers` into the workspace). */
+/* Launches the requested phases.  `layers` is the host table filled by kvc_plan(); the score /
+ * select / gather kernels receive it by value in their kernel arguments (no copy is enqueued).
+ * `layers_dev` is only used by the opt-in fused kernel (KVC_FUSED=1): a device copy of the table
+ * (e.g. at workspace + info.desc_offset) already stream-ordered with this launch, or NULL to let
+ * the library enqueue that copy itself.  Pass NULL. */
 int kvc_launch(const kvc_params_t* params, const kvc_layer_t* layers,
                const kvc_layer_t* layers_dev, int num_layers, void* workspace,
                size_t workspace_bytes, kvc_stream_t stream);

@@ -212,3 +212,17 @@ def test_abi_adversarial_depth_limit(mode):
         else:  # ascending topk == torch.topk(-x): use the oracle's topk on negated values
             ref = np.sort(oracle.topk_indices(-nrm, k), axis=-1)
         np.testing.assert_array_equal(idx, ref, err_msg=f"mode={mode} k={k}")
+
+
+@pytest.mark.parametrize("launch_path", ["kernels"], indirect=True)
+def test_more_layers_than_one_argument_chunk(launch_path):
+    """Layer tables travel by value in chunks of 64 layers: 150 layers of mixed lengths (some
+    untouched, some selecting) in one call, every layer checked against the oracle."""
+    from kvcompress.methods import h2o_l2_compress
+    layers = [(prng.gen_keys(300 + i, (1, 2, 100 + 7 * i, 64), "bf16", "few"),
+               prng.gen_values(300 + i, (1, 2, 100 + 7 * i, 64), "bf16")) for i in range(150)]
+    kw = dict(start_size=4, heavy_hitter_size=40, recent_size=60, skip_layers=[3, 77])
+    out = h2o_l2_compress([(to_dev(k), to_dev(v)) for k, v in layers], **kw)
+    ref = oracle.h2o_l2_compress(layers, **kw)
+    for li, ((ko, vo), (rk, rv, _)) in enumerate(zip(out, ref)):
+        assert np.array_equal(to_np(ko), rk) and np.array_equal(to_np(vo), rv), li
