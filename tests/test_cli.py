@@ -1,0 +1,63 @@
+"""scripts/benchmark.py (the reference CLI surface over this package): method configurations
+match the reference's build_methods_config for the same command lines (golden, generated from
+the unmodified reference by tests/golden/gen_cli_configs.py), and the CLI runs end to end on a
+random-weight model (offline)."""
+import importlib.util
+import json
+import os
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "cs3602-llm-inference-acceleration_amd", "scripts", "benchmark.py")
+GOLD = json.load(open(os.path.join(ROOT, "tests", "golden", "cli_configs.json")))
+
+
+def _cli():
+    spec = importlib.util.spec_from_file_location("kvc_cli", CLI)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@pytest.mark.parametrize("case", GOLD, ids=[" ".join(c["argv"]) for c in GOLD])
+def test_methods_config_matches_reference(case):
+    mod = _cli()
+    args = mod.build_parser().parse_args(case["argv"])
+    got = [{"name": m["name"],
+            "fn": None if m["compress_fn"] is None else m["compress_fn"].__name__,
+            "kwargs": m["kwargs"]} for m in mod.build_methods_config(args)]
+    assert got == case["methods"]
+
+
+def test_requires_a_method():
+    mod = _cli()
+    with pytest.raises(SystemExit):
+        mod.main([])
+
+
+def _small_run(mod, extra):
+    return mod.main(["--random_model", "pythia-tiny", "--synthetic_text", "--num_samples", "1",
+                     "--max_tokens", "80", "--max_new_tokens", "4", "--num_warmup", "1"] + extra)
+
+
+def test_baseline_runs_offline_on_cpu(capsys):
+    mod = _cli()
+    res = _small_run(mod, ["--compare_new"])  # the reference's --compare_new adds only baseline
+    assert [r["method"] for r in res] == ["baseline"]
+    assert np.isfinite(res[0]["perplexity"]) and res[0]["final_cache_size"] == 79
+    assert "Benchmark completed!" in capsys.readouterr().out
+
+
+@pytest.mark.gpu
+def test_cli_end_to_end_on_gpu(capsys):
+    mod = _cli()
+    res = _small_run(mod, ["--method", "fix_size_l2", "--fix_kv_sizes", "32",
+                           "--keep_ratios", "0.5", "--skip_layers", "0"])
+    names = [r["method"] for r in res]
+    assert names == ["baseline", "recent_only_32", "fix32_keep_low_kr=0.5"]
+    for r in res:
+        assert np.isfinite(r["perplexity"])
+    assert res[1]["final_cache_size"] == 32 and res[2]["final_cache_size"] == 32
+    assert "Benchmark completed!" in capsys.readouterr().out
