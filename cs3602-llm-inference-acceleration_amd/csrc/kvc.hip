@@ -20,6 +20,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "kvc.h"
 #include "kvc_common.h"
 #include "kvc_serial.h"
@@ -31,7 +33,8 @@ constexpr int kScoreThreads = 256;
 constexpr int kScoreWaves = kScoreThreads / 64;
 constexpr int kSelThreads = 1024;
 constexpr int kSelWaves = kSelThreads / 64;
-constexpr int kZoneMax = 16384;  // longest zone whose keys fit the select kernel's LDS
+constexpr int kZoneMax = 16384;        // longest zone whose selection runs from LDS
+constexpr int kZoneMaxGlobal = 65536;  // longest zone at all (u16 positions; global scratch)
 constexpr int kWaveSeg = 128;    // default: segments this short are finished by one wave
 constexpr int kGatherThreads = 256;
 constexpr int kGatherTokens = 64;  // output tokens per gather block
@@ -250,12 +253,29 @@ struct SelScalars {
   int fnan[kSelWaves];
 };
 
-// rank -> position tables (1-based); the last 64 entries of each are per-lane sinks for the
-// stores of lanes that have nothing to record (branch-free scatter)
-constexpr int kSposLen = kZoneMax + 8 + 64;     // s ranks (<= n)
-constexpr int kGposLen = kZoneMax / 2 + 8 + 64; // g ranks of the m <= (n-1)/2 swapped ge
+// Selection arrays for zones of up to n_cap positions:
+//   key[n_cap] | idx[n_cap] (u16) | 64 sinks | spos[n_cap + 8] | 64 sinks | gpos[n_cap/2 + 8]
+// spos / gpos are the s / g rank -> position tables (1-based; m <= (n-1)/2 swapped pairs); the
+// 64 entries before each are per-lane sinks for lanes with nothing to record (branch-free
+// scatter).  In LDS for n_cap = kZoneMax; in a per-row global scratch for longer zones.
+__host__ __device__ constexpr size_t sel_bytes(int n_cap, int key_size) {
+  return (size_t)n_cap * key_size + (size_t)n_cap * 2 + (size_t)(64 + n_cap + 8) * 2 +
+         (size_t)(64 + n_cap / 2 + 8) * 2;
+}
 template <typename KeyT>
-constexpr int kSelLdsBytes = kZoneMax * (int)sizeof(KeyT) + kZoneMax * 2 + (kSposLen + kGposLen) * 2;
+constexpr int kSelLdsBytes = (int)sel_bytes(kZoneMax, (int)sizeof(KeyT));
+template <typename KeyT>
+struct SelArrays {
+  KeyT* key;
+  uint16_t* idx;
+  uint16_t* spos;
+  uint16_t* gpos;
+  __device__ SelArrays(char* base, int n_cap)
+      : key(reinterpret_cast<KeyT*>(base)),
+        idx(reinterpret_cast<uint16_t*>(base + (size_t)n_cap * sizeof(KeyT))),
+        spos(idx + n_cap + 64),
+        gpos(spos + n_cap + 8 + 64) {}
+};
 
 __device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
 __device__ __forceinline__ uint64_t lanemask_le(int lane) {
@@ -377,10 +397,10 @@ __device__ __forceinline__ int mbcnt(uint64_t mask, int base) {
 // 64 positions.
 template <typename KeyT, int NT, int JM>
 __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_t* spos,
-                                               SelScalars<KeyT>& sc, int lo, int hi,
-                                               uint64_t* acc) {
+                                               uint16_t* gpos, SelScalars<KeyT>& sc, int lo,
+                                               int hi, uint64_t* acc) {
   constexpr int NW = NT / 64;
-  uint16_t* gpos = spos + kSposLen;
+  typedef typename std::conditional<(JM > 32), uint64_t, uint32_t>::type MaskT;
   const int lane = threadIdx.x & 63;
   const int wid = (NT == 64) ? 0 : uni((int)(threadIdx.x >> 6));
   const int tid = wid * 64 + lane;
@@ -406,34 +426,42 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
   }
   const uint32_t p = (ch == a) ? ka : (ch == b) ? kb : kc;
   // ---- P1: ge/le flags (one bit per j in gem/lem), wave counts ----
-  uint32_t gem = 0, lem = 0;
-  uint32_t kv[JM];
+  MaskT gem = 0, lem = 0;
+  constexpr int JB = JM < 16 ? JM : 16;  // keys loaded in batches of JB per lane
 #pragma unroll
-  for (int j = 0; j < JM; ++j) kv[j] = (uint32_t)key[min(pos0 + j * 64, hi - 1)];  // batched
+  for (int j0 = 0; j0 < JM; j0 += JB) {
+    if (j0 >= J) break;
+    uint32_t kv[JB];
 #pragma unroll
-  for (int j = 0; j < JM; ++j) {
-    if (j >= J) break;
-    const int pos = pos0 + j * 64;
-    const bool inb = pos < hi;
-    const uint32_t kk = (pos == ch) ? klo : kv[j];
-    gem |= (inb && kk >= p) ? (1u << j) : 0u;
-    lem |= (inb && kk <= p) ? (1u << j) : 0u;
+    for (int q = 0; q < JB; ++q) kv[q] = (uint32_t)key[min(pos0 + (j0 + q) * 64, hi - 1)];
+#pragma unroll
+    for (int q = 0; q < JB; ++q) {
+      const int j = j0 + q;
+      if (j >= J) break;
+      const int pos = pos0 + j * 64;
+      const bool inb = pos < hi;
+      const uint32_t kk = (pos == ch) ? klo : kv[q];
+      gem |= (inb && kk >= p) ? ((MaskT)1 << j) : (MaskT)0;
+      lem |= (inb && kk <= p) ? ((MaskT)1 << j) : (MaskT)0;
+    }
   }
   // wave counts: per-lane popcounts, one packed 64-lane sum (row scans + 4 readlanes)
-  const int rs = row_scan16(__builtin_popcount(gem) | (__builtin_popcount(lem) << 16));
+  const int rs = row_scan16(__popcll((uint64_t)gem) | (__popcll((uint64_t)lem) << 16));
   const int cnt = __builtin_amdgcn_readlane(rs, 15) + __builtin_amdgcn_readlane(rs, 31) +
                   __builtin_amdgcn_readlane(rs, 47) + __builtin_amdgcn_readlane(rs, 63);
-  const int cge = cnt & 0xFFFF, cle = cnt >> 16;  // <= 1024 each
+  const int cge = cnt & 0xFFFF, cle = (int)((uint32_t)cnt >> 16);  // <= 64 * JM each
   int ge_before = 0, le_before = 0, tot_le = cle;
   if constexpr (NW > 1) {
     static_assert(NW <= 16, "cross-wave scans use one 16-lane DPP row");
-    if (lane == 0) sc.wa[wid] = cge | (cle << 16);  // per-wave counts <= 1024: packed sums
+    if (lane == 0)  // sums < 2^16 (positions < 65536): packed
+      sc.wa[wid] = (int)((uint32_t)cge | ((uint32_t)cle << 16));
     __syncthreads();  // B_a
     const int scan = row_scan16(lane < NW ? sc.wa[lane] : 0);
-    const int before = wid ? __builtin_amdgcn_readlane(scan, wid - 1) : 0;
-    ge_before = before & 0xFFFF;
-    le_before = before >> 16;
-    tot_le = __builtin_amdgcn_readlane(scan, NW - 1) >> 16;
+    // unpack unsigned: the le half reaches bit 31 for segments longer than 32767 positions
+    const uint32_t before = wid ? (uint32_t)__builtin_amdgcn_readlane(scan, wid - 1) : 0u;
+    ge_before = (int)(before & 0xFFFFu);
+    le_before = (int)(before >> 16);
+    tot_le = (int)((uint32_t)__builtin_amdgcn_readlane(scan, NW - 1) >> 16);
   }
   KVC_TICK(t1);
   // ---- P2: s rank table, swap count m, g_{m+1} (stores only) ----
@@ -442,14 +470,14 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
 #pragma unroll
   for (int j = 0; j < JM; ++j) {
     if (j >= J) break;
-    const bool ge = (gem >> j) & 1u, le = (lem >> j) & 1u;
+    const bool ge = (gem >> j) & 1, le = (lem >> j) & 1;
     const uint64_t bg = __builtin_amdgcn_ballot_w64(ge), bl = __builtin_amdgcn_ballot_w64(le);
     const int A = mbcnt(bg, rge);                 // ge positions before this one
     const int lin = mbcnt(bl, rle) + (le ? 1 : 0);  // le positions in [lo+1, pos]
     const bool cond = A + lin < tot_le;
     const uint16_t pj = (uint16_t)(pos0 + j * 64);
-    spos[le ? tot_le - lin + 1 : kSposLen - 64 + lane] = pj;
-    gpos[(ge && cond) ? A + 1 : kGposLen - 64 + lane] = pj;  // swapped: rank A + 1 <= m
+    spos[le ? tot_le - lin + 1 : lane - 64] = pj;
+    gpos[(ge && cond) ? A + 1 : lane - 64] = pj;  // swapped: rank A + 1 <= m
     const uint64_t bc = __builtin_amdgcn_ballot_w64(cond);
     nsw += __popcll(bg & bc);
     const uint64_t bf = bg & ~bc;  // first unswapped ge: positions grow with j, so min = first
@@ -459,7 +487,8 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
   }
   int msw, gnext;
   if constexpr (NW > 1) {
-    if (lane == 0) sc.wm[wid] = nsw | ((ff == kBig ? 0xFFFF : ff) << 16);  // positions < 2^14
+    if (lane == 0)  // ff < 65535
+      sc.wm[wid] = (int)((uint32_t)nsw | ((uint32_t)(ff == kBig ? 0xFFFF : ff) << 16));
     __syncthreads();  // B_b
     const uint32_t x = lane < NW ? (uint32_t)sc.wm[lane] : 0xFFFF0000u;
     msw = __builtin_amdgcn_readlane(row_scan16((int)(x & 0xFFFFu)), NW - 1);
@@ -529,12 +558,13 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
 //   g_t < s_t  <=>  A(g_t) + Lin(g_t) < tot_le
 // so m is counted in the same pass that scatters the s rank -> position table (spos).
 // Positions are laid out j-major (lane + 64*j within a wave's stripe) so flags are wave ballots;
-// each level runs a body specialised on its positions-per-lane bound (1..16).
+// each level runs a body specialised on its positions-per-lane bound (1..16, or 64 for the
+// global-memory variant of zones longer than kZoneMax).
 // Returns 0 when the first-k set is final, 1 when the block hands a short segment to one wave.
-template <typename KeyT, int NT>
-__device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, SelScalars<KeyT>& sc, int k,
-                         bool topk, int thr, int& lo, int& hi, int& depth, int& level,
-                         int wave_seg, uint64_t* acc = nullptr) {
+template <typename KeyT, int NT, int MAXJ>
+__device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, uint16_t* gpos,
+                         SelScalars<KeyT>& sc, int k, bool topk, int thr, int& lo, int& hi,
+                         int& depth, int& level, int wave_seg, uint64_t* acc = nullptr) {
   const int tid = (NT == 64) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   while (true) {
     if (lo == k || hi == k) return 0;  // a partition boundary sits at k: the set is final
@@ -564,15 +594,21 @@ __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, SelScalars<Ke
     const uint64_t tl0 = __builtin_amdgcn_s_memtime();
 #endif
     if (J <= 1)
-      cut = partition_level<KeyT, NT, 1>(key, idx, spos, sc, lo, hi, acc);
+      cut = partition_level<KeyT, NT, 1>(key, idx, spos, gpos, sc, lo, hi, acc);
     else if (J <= 2)
-      cut = partition_level<KeyT, NT, 2>(key, idx, spos, sc, lo, hi, acc);
+      cut = partition_level<KeyT, NT, 2>(key, idx, spos, gpos, sc, lo, hi, acc);
     else if (J <= 4)
-      cut = partition_level<KeyT, NT, 4>(key, idx, spos, sc, lo, hi, acc);
+      cut = partition_level<KeyT, NT, 4>(key, idx, spos, gpos, sc, lo, hi, acc);
     else if (J <= 8)
-      cut = partition_level<KeyT, NT, 8>(key, idx, spos, sc, lo, hi, acc);
+      cut = partition_level<KeyT, NT, 8>(key, idx, spos, gpos, sc, lo, hi, acc);
+    else if (MAXJ <= 16 || J <= 16)
+      cut = partition_level<KeyT, NT, 16>(key, idx, spos, gpos, sc, lo, hi, acc);
+    else if (J <= 32)
+      cut = partition_level<KeyT, NT, (MAXJ < 32 ? 16 : 32)>(key, idx, spos, gpos, sc, lo, hi,
+                                                               acc);
     else
-      cut = partition_level<KeyT, NT, 16>(key, idx, spos, sc, lo, hi, acc);
+      cut = partition_level<KeyT, NT, (MAXJ < 64 ? 16 : 64)>(key, idx, spos, gpos, sc, lo, hi,
+                                                               acc);
 #ifdef KVC_STAMPS
     // per block level (first 8): cycles, and segment length  (slots 16.. of the row)
     if (acc && NT > 64 && tid == 0 && level < 7) {
@@ -589,26 +625,28 @@ __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, SelScalars<Ke
   }
 }
 
-// Reference-exact selection for one (layer, b, h) row whose zone norms are at `nrow`; LDS in
-// `smem` (key | idx | spos, see select_kernel) and `sc`.  Emits the kept zone-local indices in
+// Reference-exact selection for one (layer, b, h) row whose zone norms are at `nrow`; working
+// arrays at `arrays` (SelArrays layout for n_cap positions: LDS, or a global scratch row for
+// zones longer than kZoneMax) and scalars in `sc`.  Emits the kept zone-local indices in
 // ascending order to `out` (global int32) or, with TO_LDS, to `sel` (LDS u16, may alias
 // the key region: keys are dead by then).
-template <int DT, bool TO_LDS>
+template <int DT, bool TO_LDS, int MAXN>
 __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, int order, int algo,
                             const char* __restrict__ nrow, int32_t* out, uint16_t* sel,
-                            char* smem, SelScalars<typename DTypeTraits<DT>::key_t>& sc,
+                            char* arrays, int n_cap,
+                            SelScalars<typename DTypeTraits<DT>::key_t>& sc,
                             int wave_seg, uint64_t* stamps) {
   typedef typename DTypeTraits<DT>::key_t KeyT;
   constexpr int ESZ = DTypeTraits<DT>::esz;
-  constexpr int KEY_B = kZoneMax * (int)sizeof(KeyT);
-  constexpr int IDX_B = kZoneMax * 2;
-  KeyT* key = reinterpret_cast<KeyT*>(smem);
-  uint16_t* idx = reinterpret_cast<uint16_t*>(smem + KEY_B);
-  uint16_t* spos = reinterpret_cast<uint16_t*>(smem + KEY_B + IDX_B);
+  constexpr int MAXJ = (MAXN + kSelThreads - 1) / kSelThreads;  // positions per lane, level 0
+  const SelArrays<KeyT> A(arrays, n_cap);
+  KeyT* key = A.key;
+  uint16_t* idx = A.idx;
+  uint16_t* spos = A.spos;
   KVC_STAMP(0);
   const int n = ly->zone_len;
   const int k = ly->n_select;
-  if (k <= 0 || n <= 0 || n > kZoneMax) return;
+  if (k <= 0 || n <= 0 || n > MAXN || n > n_cap) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (k >= n) {  // keep everything (e.g. h2o_l2 when the middle is no longer than heavy_hitter)
     for (int i = tid; i < n; i += kSelThreads) {
@@ -630,17 +668,18 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
     // 16-B loads, all issued before the first use (norm rows are padded to 64 elements, so a
     // whole vector past n stays inside the row); keys/indices written as 16-B LDS stores
     constexpr int VEC = 16 / ESZ;
-    constexpr int MAXV = (kZoneMax / VEC + kSelThreads - 1) / kSelThreads;
+    constexpr int MAXV = (kZoneMax / VEC + kSelThreads - 1) / kSelThreads;  // per batch
     const int nvec = (n + VEC - 1) / VEC;
+    for (int v0 = 0; v0 < nvec; v0 += MAXV * kSelThreads) {  // one batch for n <= kZoneMax
     uint4 buf[MAXV];
 #pragma unroll
     for (int q = 0; q < MAXV; ++q) {
-      const int v = tid + q * kSelThreads;
+      const int v = v0 + tid + q * kSelThreads;
       if (v < nvec) buf[q] = reinterpret_cast<const uint4*>(nrow)[v];
     }
 #pragma unroll
     for (int q = 0; q < MAXV; ++q) {
-      const int v = tid + q * kSelThreads;
+      const int v = v0 + tid + q * kSelThreads;
       if (v < nvec) {
         const uint32_t w[4] = {buf[q].x, buf[q].y, buf[q].z, buf[q].w};
         uint32_t kw[4], iw[4];
@@ -662,6 +701,7 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
                          (uint32_t)(v * 4 + 2) | ((uint32_t)(v * 4 + 3) << 16));
         }
       }
+    }
     }
   }
   __syncthreads();
@@ -685,11 +725,12 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
         for (int q = 0; q < 27; ++q) accb[q] = 0;
     }
 #endif
-    const int st = run_chain<KeyT, kSelThreads>(key, idx, spos, sc, k, topk, thr, lo, hi, depth,
-                                                level, wave_seg, accb);
+    const int st = run_chain<KeyT, kSelThreads, MAXJ>(key, idx, spos, A.gpos, sc, k, topk, thr,
+                                                      lo, hi, depth, level, wave_seg, accb);
     KVC_STAMP(2);
     if (st == 1 && wid == 0)
-      run_chain<KeyT, 64>(key, idx, spos, sc, k, topk, thr, lo, hi, depth, level, wave_seg, accw);
+      run_chain<KeyT, 64, 16>(key, idx, spos, A.gpos, sc, k, topk, thr, lo, hi, depth, level,
+                              wave_seg, accw);
   }
   __syncthreads();
   KVC_STAMP(3);
@@ -702,12 +743,12 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
   __syncthreads();
   const int J = (n + kSelThreads - 1) / kSelThreads;
   const int wbeg = wid * J * 64;
-  uint32_t fm = 0;
+  uint64_t fm = 0;  // J <= 64
   int c = 0;
   for (int j = 0; j < J; ++j) {
     const int pos = wbeg + j * 64 + lane;
     const bool f = pos < n && flag[pos] != 0;
-    fm |= (uint32_t)f << j;
+    fm |= (uint64_t)f << j;
     c += __popcll(__ballot(f));
   }
   if (lane == 0) sc.wa[wid] = c;
@@ -715,7 +756,7 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
   int run = 0;
   for (int w = 0; w < wid; ++w) run += sc.wa[w];
   for (int j = 0; j < J; ++j) {
-    const bool f = (fm >> j) & 1u;
+    const bool f = (fm >> j) & 1;
     const uint64_t bf = __ballot(f);
     if (f) {
       const int r = run + __popcll(bf & lanemask_lt(lane));
@@ -741,9 +782,30 @@ __global__ void __launch_bounds__(kSelThreads)
   __shared__ SelScalars<KeyT> sc;
   const kvc_layer_t* ly = T.l + blockIdx.x / BH;
   const int row = ly->row0 + (int)(blockIdx.x % BH);  // global workspace row
-  select_body<DT, false>(ly, order, algo, norms + (int64_t)row * norm_stride * ESZ,
-                         out_idx + (int64_t)row * idx_stride, nullptr, smem, sc, wave_seg,
-                         stamps);
+  select_body<DT, false, kZoneMax>(ly, order, algo, norms + (int64_t)row * norm_stride * ESZ,
+                                   out_idx + (int64_t)row * idx_stride, nullptr, smem, kZoneMax,
+                                   sc, wave_seg, stamps);
+}
+
+// Zones longer than kZoneMax (up to kZoneMaxGlobal): the same selection with its arrays in a
+// per-row global scratch (L2 / Infinity-Cache resident; a workgroup barrier orders the
+// workgroup's global accesses like LDS ones -- all its waves share one CU's L1).
+template <int DT>
+__global__ void __launch_bounds__(kSelThreads)
+    select_global_kernel(const LayerChunk T, int BH, int order, int algo,
+                         const char* __restrict__ norms, int64_t norm_stride,
+                         int32_t* __restrict__ out_idx, int64_t idx_stride, int wave_seg,
+                         char* __restrict__ scratch, int64_t scratch_row_bytes, int n_cap) {
+  typedef typename DTypeTraits<DT>::key_t KeyT;
+  constexpr int ESZ = DTypeTraits<DT>::esz;
+  __shared__ SelScalars<KeyT> sc;
+  const kvc_layer_t* ly = T.l + blockIdx.x / BH;
+  const int row = ly->row0 + (int)(blockIdx.x % BH);
+  select_body<DT, false, kZoneMaxGlobal>(ly, order, algo,
+                                         norms + (int64_t)row * norm_stride * ESZ,
+                                         out_idx + (int64_t)row * idx_stride, nullptr,
+                                         scratch + (int64_t)row * scratch_row_bytes, n_cap, sc,
+                                         wave_seg, nullptr);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1019,8 +1081,8 @@ __global__ void __launch_bounds__(kSelThreads)
       __syncthreads();
       KVC_TL(r * 4 + 1);
       uint16_t* sel = reinterpret_cast<uint16_t*>(smem);  // key region, dead after the chain
-      select_body<DT, true>(ly, order, algo, norms + (int64_t)r * norm_stride * ESZ, nullptr,
-                            sel, smem, sc, wave_seg, nullptr);
+      select_body<DT, true, kZoneMax>(ly, order, algo, norms + (int64_t)r * norm_stride * ESZ,
+                                      nullptr, sel, smem, kZoneMax, sc, wave_seg, nullptr);
       __syncthreads();
       KVC_TL(r * 4 + 2);
       gather_row<DT, NC>(ly, row, H, sel);
@@ -1041,6 +1103,10 @@ __global__ void __launch_bounds__(kSelThreads)
 static inline int esize(int dtype) { return dtype == KVC_BF16 ? 2 : 4; }
 static inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+// one row of the global selection scratch (SelArrays for n_cap positions), 256-B aligned rows
+static inline size_t sel_scratch_row_bytes(int n_cap, int dtype) {
+  return round_up(sel_bytes(n_cap, dtype == KVC_BF16 ? 2 : 4), 256);
+}
 
 static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_plan_info_t* info,
                      bool fill) {
@@ -1068,7 +1134,7 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
     const int64_t n_out = (int64_t)y.sink_len + y.n_select + y.tail_len;
     if (n_out > 0x7FFFFFFF || 2 * BH * n_out * nc > 0x7FFFFFFF) return KVC_E_ARG;
     const bool needs_select = y.n_select > 0 && y.n_select < y.zone_len;
-    if (needs_select && y.zone_len > kZoneMax) return KVC_E_TOO_LONG;
+    if (needs_select && y.zone_len > kZoneMaxGlobal) return KVC_E_TOO_LONG;
     if (n_out > 0) {
       if (!y.k || !y.v || !y.k_out || !y.v_out) return KVC_E_ARG;
       if (!aligned16(y.k) || !aligned16(y.v) || !aligned16(y.k_out) || !aligned16(y.v_out))
@@ -1112,6 +1178,8 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
     off = round_up(off + (size_t)rows * info->norm_row_stride * es, 256);
     info->index_offset = off;
     off = round_up(off + (size_t)rows * info->index_row_stride * 4, 256);
+    if (max_zone > kZoneMax)  // selection scratch rows for zones longer than the LDS limit
+      off += (size_t)rows * sel_scratch_row_bytes((int)info->norm_row_stride, p->dtype);
 #ifdef KVC_STAMPS
     off += (size_t)rows * 256;  // diagnostic stamp slots (32 x u64 per select row)
 #endif
@@ -1176,7 +1244,7 @@ extern "C" {
 
 int kvc_version(void) { return KVC_ABI_VERSION; }
 size_t kvc_layer_struct_size(void) { return sizeof(kvc_layer_t); }
-int kvc_max_zone_len(void) { return kvc::kZoneMax; }
+int kvc_max_zone_len(void) { return kvc::kZoneMaxGlobal; }
 
 const char* kvc_status_string(int s) {
   switch (s) {
@@ -1229,7 +1297,8 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
   // 128/256-byte rows (wider rows need more than the 128 VGPRs a 1024-thread workgroup allows).
   // It overlaps selection with the key stream, but on the headline workload the three-kernel
   // path with non-temporal streams is faster, so that is the default.
-  bool fused = p->phases == KVC_PHASE_ALL && !p->external_index && (nc == 8 || nc == 16);
+  bool fused = p->phases == KVC_PHASE_ALL && !p->external_index && (nc == 8 || nc == 16) &&
+               info.norm_row_stride <= kZoneMax;  // LDS-resident selection only
   const char* fe = getenv("KVC_FUSED");
   fused = fused && fe && strcmp(fe, "1") == 0;
   if (fused) {
@@ -1280,10 +1349,12 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
     memcpy(T.l, layers + c0, (size_t)cn * sizeof(kvc_layer_t));
     const int64_t tile_base = layers[c0].tile0;
     const int64_t tile_end = c0 + cn < nl ? (int64_t)layers[c0 + cn].tile0 : info.score_tiles;
-    bool sel = false;
+    bool sel = false, long_zone = false;
     int64_t max_out = 0;
     for (int l = c0; l < c0 + cn; ++l) {
       sel |= layers[l].n_select > 0;
+      long_zone |= layers[l].n_select > 0 && layers[l].n_select < layers[l].zone_len &&
+                   layers[l].zone_len > kZoneMax;
       max_out = layers[l].n_out > max_out ? layers[l].n_out : max_out;
     }
     if ((p->phases & KVC_PHASE_SCORE) && tile_end > tile_base && !p->external_index) {
@@ -1294,7 +1365,21 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
         dispatch_nc<KVC_F32>(nc, true, T, cn, H, BH, tile_base, tile_end - tile_base, norms,
                              info.norm_row_stride, idx, info.index_row_stride, s);
     }
-    if ((p->phases & KVC_PHASE_SELECT) && sel && !p->external_index) {
+    if ((p->phases & KVC_PHASE_SELECT) && sel && !p->external_index && long_zone) {
+      const dim3 grid((unsigned)(cn * BH)), block(kSelThreads);
+      const int n_cap = (int)info.norm_row_stride;
+      char* scratch = w + round_up(info.index_offset +
+                                   (size_t)info.rows * info.index_row_stride * 4, 256);
+      const int64_t rb = (int64_t)sel_scratch_row_bytes(n_cap, p->dtype);
+      if (p->dtype == KVC_BF16)
+        hipLaunchKernelGGL(select_global_kernel<KVC_BF16>, grid, block, 0, s, T, BH, p->order,
+                           p->algo, norms, info.norm_row_stride, idx, info.index_row_stride,
+                           wave_seg, scratch, rb, n_cap);
+      else
+        hipLaunchKernelGGL(select_global_kernel<KVC_F32>, grid, block, 0, s, T, BH, p->order,
+                           p->algo, norms, info.norm_row_stride, idx, info.index_row_stride,
+                           wave_seg, scratch, rb, n_cap);
+    } else if ((p->phases & KVC_PHASE_SELECT) && sel && !p->external_index) {
       const dim3 grid((unsigned)(cn * BH)), block(kSelThreads);
       uint64_t* st = stamps ? stamps + (size_t)layers[c0].row0 * 32 : nullptr;
       if (p->dtype == KVC_BF16)

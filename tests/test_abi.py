@@ -32,7 +32,7 @@ def test_struct_layout():
     assert ctypes.sizeof(N.Params) == 32
     assert ctypes.sizeof(N.PlanInfo) == 80
     assert L.kvc_version() == 1
-    assert L.kvc_max_zone_len() == 16384
+    assert L.kvc_max_zone_len() == 65536
 
 
 def _layer(S, zs, zl, k, sink=0, ts=0, tl=0, ptr=4096):
@@ -81,14 +81,29 @@ def test_plan_rejects_bad_layers():
         (_layer(100, 0, 100, 101), -1),                # selecting more than the zone
         (_layer(100, 0, 100, 10, ts=95, tl=10), -1),   # tail past the end
         (_layer(100, 0, 100, 10, ptr=4100), -4),       # misaligned pointer
-        (_layer(20000, 0, 20000, 10), -5),             # zone longer than LDS-resident limit
+        (_layer(70000, 0, 70000, 10), -5),             # zone longer than 65536 positions
     ]
     for t, code in cases:
         rc, _ = N.plan(_params(), np.array([t], dtype=N.LAYER_DTYPE))
         assert rc == code, (t, rc)
-    # select-all and pure-copy layers may be longer than the LDS limit (no selection runs)
-    rc, _ = N.plan(_params(), np.array([_layer(20000, 0, 20000, 20000)], dtype=N.LAYER_DTYPE))
+    # select-all and pure-copy layers may be longer still (no selection runs)
+    rc, _ = N.plan(_params(), np.array([_layer(70000, 0, 70000, 70000)], dtype=N.LAYER_DTYPE))
     assert rc == 0
+
+
+def test_plan_long_zone_gets_global_scratch():
+    """Zones longer than the LDS limit (16384) select from a per-row global scratch."""
+    short = np.array([_layer(16384, 0, 16384, 512)], dtype=N.LAYER_DTYPE)
+    long_ = np.array([_layer(40000, 0, 40000, 512)], dtype=N.LAYER_DTYPE)
+    rc0, i0 = N.plan(_params(), short)
+    rc1, i1 = N.plan(_params(), long_)
+    assert rc0 == 0 and rc1 == 0
+    n_cap = 40000 + (-40000 % 64)
+    row = n_cap * 2 + n_cap * 2 + (64 + n_cap + 8) * 2 + (64 + n_cap // 2 + 8) * 2
+    row += -row % 256
+    idx_end = i1.index_offset + 32 * i1.index_row_stride * 4
+    idx_end += -idx_end % 256
+    assert i1.workspace_bytes == idx_end + 32 * row
 
 
 def test_status_strings():

@@ -226,3 +226,27 @@ def test_more_layers_than_one_argument_chunk(launch_path):
     ref = oracle.h2o_l2_compress(layers, **kw)
     for li, ((ko, vo), (rk, rv, _)) in enumerate(zip(out, ref)):
         assert np.array_equal(to_np(ko), rk) and np.array_equal(to_np(vo), rv), li
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_zones_longer_than_lds_limit(dtype):
+    """Zones > 16384 positions select from the global-scratch variant (up to 65536; the
+    cross-wave counts of segments > 32767 positions use the packed counters' top bit)."""
+    from kvcompress.methods import fix_size_l2_compress, l2_compress, snapkv_lite_compress
+    for S, variant in ((20000, "few"), (40000, "normal"), (65536, "equal")):
+        K = prng.gen_keys(4000 + S, (1, 2, S, 64), dtype, variant)
+        V = prng.gen_values(4000 + S, (1, 2, S, 64), dtype)
+        kv = [(to_dev(K), to_dev(V))]
+        for fn, ref, kw in (
+                (fix_size_l2_compress, oracle.fix_size_l2_compress,
+                 dict(fix_kv_size=700, keep_ratio=0.25, skip_layers=[])),
+                (fix_size_l2_compress, oracle.fix_size_l2_compress,
+                 dict(fix_kv_size=S // 2, strategy="keep_high", skip_layers=[])),
+                (snapkv_lite_compress, oracle.snapkv_lite_compress,
+                 dict(observation_window=32, keep_size=S // 3, skip_layers=[])),
+                (l2_compress, oracle.l2_compress,
+                 dict(keep_ratio=0.8, prune_after=100, skip_layers=[]))):
+            out = fn(list(kv), **kw)
+            rk, rv, _ = ref([(K, V)], **kw)[0]
+            assert np.array_equal(to_np(out[0][0]), rk), (S, fn.__name__, kw)
+            assert np.array_equal(to_np(out[0][1]), rv), (S, fn.__name__, kw)
