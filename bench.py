@@ -7,6 +7,10 @@ Inputs are resident in HBM before the timed region.  Multi-GPU: one process per 
 each rank owns 32 layers of a 32*N-layer stack (layers sharded, no collectives on the data
 path; weak scaling); a barrier + synchronize brackets the timed region and the max over ranks
 is reported.  Prints ONE JSON line on rank 0.
+
+`--workload` selects one of the other BASELINE / SURVEY §8(d) configurations (same contract, same
+JSON line; the default is the headline).  `--layers-total L` shards an L-layer model over the
+ranks instead (strong scaling, global layer indices; e.g. cfg4: h2o_l2, 32 layers over 8 GPUs).
 """
 import argparse
 import json
@@ -25,6 +29,29 @@ LAYERS, B, H, S, D = 32, 1, 32, 16384, 128
 FIX = 512
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
+# name -> (method, kwargs, seq_len, head_dim, what).  The headline is BASELINE.json's metric
+# config; the others are its configs[1..4] at the §8(d) geometries (pythia-2.8b: D=80,
+# pythia-6.9b: D=128; 32 heads, 32 layers).
+WORKLOADS = {
+    "fix512-s16384": ("fix_size_l2", dict(fix_kv_size=512, keep_ratio=0.0, strategy="keep_low"),
+                      16384, 128, "headline"),
+    "fix512-s4096": ("fix_size_l2", dict(fix_kv_size=512, keep_ratio=0.0, strategy="keep_low"),
+                     4096, 128, "cfg2 geometry of the north star ([1,32,S,128])"),
+    "fix512-s4096-d80": ("fix_size_l2", dict(fix_kv_size=512, keep_ratio=0.0,
+                                             strategy="keep_low"), 4096, 80, "cfg2, pythia-2.8b"),
+    "streaming-s16384": ("streaming_llm", dict(start_size=4, recent_size=1020), 16384, 80,
+                         "cfg3, pythia-2.8b"),
+    "h2o-s16384": ("h2o_l2", dict(start_size=4, heavy_hitter_size=64, recent_size=444), 16384, 80,
+                   "cfg4, pythia-2.8b"),
+    "snapkv-s16384": ("snapkv_lite", dict(observation_window=32, keep_size=512), 16384, 128,
+                      "cfg5, pythia-6.9b"),
+    "pyramid-s16384": ("pyramid_kv", dict(base_size=512), 16384, 128, "cfg5, pythia-6.9b"),
+    "l2-s16384": ("l2_compress", dict(keep_ratio=0.8, prune_after=100), 16384, 80,
+                  "cfg1 method (one-shot), pythia-2.8b"),
+    "adaptive-s16384": ("adaptive_l2", dict(), 16384, 128, "adaptive_l2 defaults"),
+}
+HEADLINE = "fix512-s16384"
+
 
 def algorithmic_bytes(es=2):
     """Per layer: K read over S + kept V rows read + K,V kept rows written."""
@@ -32,6 +59,26 @@ def algorithmic_bytes(es=2):
     per_layer = R * (S + FIX + 2 * FIX)
     score = B * H * S * (D * es + es)  # score kernel: K read + one norm written per position
     return per_layer, score
+
+
+def job_bytes(jobs, es):
+    """Algorithmic bytes of one call from its engine jobs (generalised): per layer
+    R = B*H*D*e and out = sink + selected + tail rows:
+      path   = R * (zone + sink + tail + 3*out)   K scored over the zone, K rows copied from the
+               sink/tail, V kept rows read, K and V out written (selected K rows not re-counted)
+      score  = B*H*zone*(D*e + e)                 K read + one norm written per scored position
+      gather = 4 * R * out                        K,V kept rows read + written
+    """
+    path = score = gather = 0
+    for j in jobs:
+        b, h, _, d = j.keys.shape
+        R = b * h * d * es
+        out = j.sink_len + j.n_select + j.tail_len
+        zone = j.zone_len if j.n_select else 0
+        path += R * (zone + j.sink_len + j.tail_len + 3 * out)
+        score += b * h * zone * (d * es + es)
+        gather += 4 * R * out
+    return {"path": path, "score": score, "gather": gather}
 
 
 PMC_FILE = "profiles/r01_v7_pmc_traffic.json"  # tools/gpu_check.sh pmc + tools/pmc_traffic.py
@@ -50,7 +97,7 @@ def pmc_traffic(kernel="kvc::score_kernel<1, 16, true>"):
         return None
 
 
-def cpu_baseline(seconds=12.0):
+def cpu_baseline(seq_len=S, head_dim=D, seconds=12.0):
     """The reference's CPU op sequence (oracle/torch_port.py) on this host's cores, bounded."""
     from oracle.torch_port import fix_size_l2_layer
     # the GPU box exposes the whole machine's CPUs but grants one GPU a 16-core share
@@ -58,17 +105,17 @@ def cpu_baseline(seconds=12.0):
     threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(0)
-    k = torch.randn(B, H, S, D, generator=g).to(torch.bfloat16)
-    v = torch.randn(B, H, S, D, generator=g).to(torch.bfloat16)
+    k = torch.randn(B, H, seq_len, head_dim, generator=g).to(torch.bfloat16)
+    v = torch.randn(B, H, seq_len, head_dim, generator=g).to(torch.bfloat16)
     fix_size_l2_layer(k, v, FIX)  # warm
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         fix_size_l2_layer(k, v, FIX)
         n += 1
     dt = time.perf_counter() - t0
-    return {"value": n * S / dt, "unit": "KV tokens/s", "cores": threads, "kind": "port",
-            "sample": f"{n} layers of fix_size_l2(512) on one [1,32,16384,128] bf16 layer "
-                      f"(torch CPU ops: norm->argsort->sort->gather), {dt:.1f}s, "
+    return {"value": n * seq_len / dt, "unit": "KV tokens/s", "cores": threads, "kind": "port",
+            "sample": f"{n} layers of fix_size_l2(512) on one [1,32,{seq_len},{head_dim}] bf16 "
+                      f"layer (torch CPU ops: norm->argsort->sort->gather), {dt:.1f}s, "
                       f"{torch.backends.cpu.get_cpu_capability()}"}
 
 
@@ -108,11 +155,31 @@ def shard_layers(num_layers_total, world, rank):
     return start, start + per + (1 if rank < extra else 0)
 
 
+def capture_jobs(step):
+    """Run one call with the engine's execute() wrapped, returning the jobs it was given."""
+    from kvcompress import _engine
+    seen, real = [], _engine.execute
+
+    def spy(jobs, *a, **kw):
+        seen.extend(jobs)
+        return real(jobs, *a, **kw)
+    _engine.execute = spy
+    try:
+        step()
+    finally:
+        _engine.execute = real
+    return seen
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default=HEADLINE, choices=sorted(WORKLOADS))
+    ap.add_argument("--layers-total", type=int, default=0,
+                    help="shard this many layers over the ranks (strong scaling); "
+                         "default: 32 layers per GPU (weak scaling)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -127,66 +194,92 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from kvcompress import _engine
-    from kvcompress.methods import fix_size_l2_compress
+    from kvcompress.methods import get_compress_fn
+
+    method, kwargs, seq_len, head_dim, what = WORKLOADS[args.workload]
+    if args.layers_total:
+        l0, l1 = shard_layers(args.layers_total, world, rank)
+        total, scaling = args.layers_total, "strong"
+    else:  # rank r owns layers [32r, 32r + 32) of a 32*N-layer stack
+        l0, l1 = LAYERS * rank, LAYERS * (rank + 1)
+        total, scaling = LAYERS * world, "weak"
+    n_layers = l1 - l0
+    extra = dict(layer_offset=l0, num_layers_total=total) if method == "pyramid_kv" else {}
+    fn = get_compress_fn(method)
 
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     layers = []
-    for _ in range(LAYERS):
-        k = torch.randn(B, H, S, D, device=dev, generator=g, dtype=torch.float32).to(torch.bfloat16)
-        v = torch.randn(B, H, S, D, device=dev, generator=g, dtype=torch.float32).to(torch.bfloat16)
+    for _ in range(n_layers):
+        k = torch.randn(B, H, seq_len, head_dim, device=dev, generator=g,
+                        dtype=torch.float32).to(torch.bfloat16)
+        v = torch.randn(B, H, seq_len, head_dim, device=dev, generator=g,
+                        dtype=torch.float32).to(torch.bfloat16)
         layers.append((k, v))
 
     def step():
-        return fix_size_l2_compress(layers, fix_kv_size=FIX, keep_ratio=0.0, strategy="keep_low",
-                                    skip_layers=[])
+        return fn(layers, skip_layers=[], **kwargs, **extra)
 
+    nbytes = job_bytes(capture_jobs(step), 2)
     # per-kernel durations: the engine splits each launch into its three kernels with HIP
     # events (recorded on the stream they run on) for the whole timed region
     timer = _engine.PhaseTimer()
     elapsed = timed_steps(step, args.steps, args.warmup, dist, torch.cuda.synchronize, dev,
                           on_start=lambda: _engine.set_phase_timer(timer))
     _engine.set_phase_timer(None)
-    dur = timer.durations_ms()
+    dur = {k: sum(v) / len(v) for k, v in timer.durations_ms().items()}
+
+    # units all ranks processed: positions scored (layers x S) per step
+    units = torch.tensor([n_layers * seq_len], dtype=torch.float64)
+    if dist:
+        units = units.to(dev)
+        dist.all_reduce(units)
+    units = float(units.item())
 
     if rank == 0:
-        per_layer, score_bytes_layer = algorithmic_bytes()
         ms_step = elapsed / args.steps * 1e3
-        tokens = LAYERS * S * args.steps * world
-        score_ms = sum(dur["score"]) / len(dur["score"])
-        score_gbps = score_bytes_layer * LAYERS / (score_ms * 1e-3) / 1e9
-        traffic = pmc_traffic()
-        path_gbps = per_layer * LAYERS / (ms_step * 1e-3) / 1e9
+        kern = max(dur, key=dur.get)  # dominant kernel of the step
+        kern_gbps = nbytes[kern] / (dur[kern] * 1e-3) / 1e9
+        headline = args.workload == HEADLINE
+        traffic = pmc_traffic() if headline and kern == "score" else None
+        path_gbps = nbytes["path"] * world / (ms_step * 1e-3) / 1e9
+        desc = {"score": "score_kernel (key L2 norms)", "select": "select_kernel",
+                "gather": "gather_kernel (segment copy)"}[kern]
+        cfg_kw = ", ".join(f"{k}={v!r}" for k, v in kwargs.items())
         res = {
             "metric": "KV tokens scored+evicted/sec at S=16384, fix_size=512; PPL delta vs ref",
-            "value": tokens / elapsed,
+            "value": units * args.steps / elapsed,
             "unit": "KV tokens/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (torch.randn, HBM-resident)",
-            "config": {"workload": "fix_size_l2_compress(fix_kv_size=512, keep_ratio=0.0, "
-                                   "strategy='keep_low', skip_layers=[]) over 32 layers of "
-                                   "K,V [1,32,16384,128] per GPU, one call per step",
-                       "layers_per_gpu": LAYERS, "seq_len": S, "heads": H, "head_dim": D,
-                       "fix_kv_size": FIX, "parallelism": f"layers sharded x{world}, no collectives"},
-            "roofline": {"bound": "hbm", "kernel": "score_kernel (key L2 norms)",
-                         "achieved": score_gbps, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
-                         "frac": score_gbps / PEAK_HBM_GBPS, "traffic": traffic,
-                         "algorithmic_bytes_per_launch": score_bytes_layer * LAYERS,
-                         "traffic_source": PMC_FILE + " (rocprofv3 --pmc)"},
+            "config": {"workload": f"{method}_compress({cfg_kw}, skip_layers=[]) over "
+                                   f"{n_layers} layers of K,V [1,{H},{seq_len},{head_dim}] per "
+                                   f"GPU, one call per step ({what})",
+                       "name": args.workload, "layers_per_gpu": n_layers,
+                       "layers_total": total, "seq_len": seq_len, "heads": H,
+                       "head_dim": head_dim,
+                       "parallelism": f"layers sharded x{world}, no collectives"},
+            "roofline": {"bound": "hbm", "kernel": desc,
+                         "achieved": kern_gbps, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                         "frac": kern_gbps / PEAK_HBM_GBPS, "traffic": traffic,
+                         "algorithmic_bytes_per_launch": nbytes[kern],
+                         "traffic_source": (PMC_FILE + " (rocprofv3 --pmc)") if traffic else None},
             "path_roofline": {"achieved": path_gbps, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                               "frac": path_gbps / PEAK_HBM_GBPS,
-                              "bytes_per_layer": per_layer},
-            "kernel_ms_per_step": {k: sum(v) / len(v) for k, v in dur.items()},
-            "tokens_evicted_per_sec": (S - FIX) * LAYERS * args.steps * world / elapsed,
+                              "bytes_per_step_per_gpu": nbytes["path"]},
+            "kernel_ms_per_step": dur,
+            "tokens_evicted_per_sec": None,
         }
-        if not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline()
+        ev = sum(kv[0].size(2) for kv in layers) - sum(kv[0].size(2) for kv in step())
+        res["tokens_evicted_per_sec"] = ev * world * args.steps / elapsed
+        if not args.no_cpu_baseline and method == "fix_size_l2":
+            res["cpu_baseline"] = cpu_baseline(seq_len, head_dim)
         print(json.dumps(res), flush=True)
     if dist:
         dist.barrier()

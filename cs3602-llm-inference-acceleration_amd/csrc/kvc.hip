@@ -33,6 +33,8 @@ constexpr int kScoreThreads = 256;
 constexpr int kScoreWaves = kScoreThreads / 64;
 constexpr int kSelThreads = 1024;
 constexpr int kSelWaves = kSelThreads / 64;
+constexpr int kSelThreadsSmall = 256;  // select workgroup for zones of up to kSmallZone
+constexpr int kSmallZone = kSelThreadsSmall * 16;
 constexpr int kZoneMax = 16384;        // longest zone whose selection runs from LDS
 constexpr int kZoneMaxGlobal = 65536;  // longest zone at all (u16 positions; global scratch)
 constexpr int kWaveSeg = 128;    // default: segments this short are finished by one wave
@@ -254,27 +256,36 @@ struct SelScalars {
 };
 
 // Selection arrays for zones of up to n_cap positions:
-//   key[n_cap] | idx[n_cap] (u16) | 64 sinks | spos[n_cap + 8] | 64 sinks | gpos[n_cap/2 + 8]
-// spos / gpos are the s / g rank -> position tables (1-based; m <= (n-1)/2 swapped pairs); the
-// 64 entries before each are per-lane sinks for lanes with nothing to record (branch-free
-// scatter).  In LDS for n_cap = kZoneMax; in a per-row global scratch for longer zones.
-__host__ __device__ constexpr size_t sel_bytes(int n_cap, int key_size) {
-  return (size_t)n_cap * key_size + (size_t)n_cap * 2 + (size_t)(64 + n_cap + 8) * 2 +
-         (size_t)(64 + n_cap / 2 + 8) * 2;
+//   key[n_cap] | idx[n_cap] (u16) | 64 sinks | spos[cap + 8] | 64 sinks | gpos[cap + 8]
+// spos / gpos are the s / g rank -> position tables (1-based) of one window of `cap` swap ranks
+// (m <= (n-1)/2 swapped pairs per level; a level with m > cap runs its swaps in windows); the 64
+// entries before each are per-lane sinks for lanes with nothing to record (branch-free scatter).
+// In LDS (dynamic, sized by the call's longest zone), or in a per-row global scratch for zones
+// longer than kZoneMax.
+__host__ __device__ constexpr size_t sel_bytes(int n_cap, int key_size, int cap) {
+  return (size_t)n_cap * key_size + (size_t)n_cap * 2 + (size_t)(64 + cap + 8) * 2 * 2;
 }
-template <typename KeyT>
-constexpr int kSelLdsBytes = (int)sel_bytes(kZoneMax, (int)sizeof(KeyT));
+// Rank-window size for an n_cap-position LDS selection.  bf16 rows of up to 16 384 positions fit
+// two workgroups per CU (<= 80 KiB each, 160 KiB LDS per CU) when the tables hold fewer than the
+// n_cap/2 ranks a level can need; levels with more swaps take a second window.  fp32 keys (and
+// short zones) get full tables.
+__host__ __device__ constexpr int sel_cap(int n_cap, int key_size) {
+  const int full = n_cap / 2 + 1;
+  const long budget = 81408L - (long)n_cap * (key_size + 2) - 4L * 72;  // bytes for the tables
+  const int fit = budget > 0 ? (int)(budget / 4) : 0;
+  return (key_size == 2 && fit < full && fit >= 1024) ? (fit & ~63) : full;
+}
 template <typename KeyT>
 struct SelArrays {
   KeyT* key;
   uint16_t* idx;
   uint16_t* spos;
   uint16_t* gpos;
-  __device__ SelArrays(char* base, int n_cap)
+  __device__ SelArrays(char* base, int n_cap, int cap)
       : key(reinterpret_cast<KeyT*>(base)),
         idx(reinterpret_cast<uint16_t*>(base + (size_t)n_cap * sizeof(KeyT))),
         spos(idx + n_cap + 64),
-        gpos(spos + n_cap + 8 + 64) {}
+        gpos(spos + cap + 8 + 64) {}
 };
 
 __device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
@@ -285,13 +296,13 @@ __device__ __forceinline__ uint64_t lanemask_le(int lane) {
 // snapkv_lite importance scores (snapkv_lite.py:96-121) computed from the row's norms and
 // written as sort keys:  m = dt(max(norms) + 1e-6);  s = dt(m - norm);
 // pooled_i = dt(sum_{window} s / pool_size) (avg_pool1d, zero pad, count_include_pad).
-template <int DT, typename KeyT>
+template <int DT, typename KeyT, int NT>
 __device__ void snapkv_keys(const char* nrow, int n, int pool_k, bool desc, KeyT* key,
                             char* tmp, SelScalars<KeyT>& sc) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   float mx = -__builtin_huge_valf();
   int has_nan = 0;
-  for (int i = tid; i < n; i += kSelThreads) {
+  for (int i = tid; i < n; i += NT) {
     const float v = load_dt<DT>(nrow, i);
     if (v != v) has_nan = 1;
     else if (v > mx) mx = v;
@@ -309,13 +320,13 @@ __device__ void snapkv_keys(const char* nrow, int n, int pool_k, bool desc, KeyT
   __syncthreads();
   mx = sc.fmax[0];
   has_nan = sc.fnan[0];
-  for (int w = 1; w < kSelWaves; ++w) {
+  for (int w = 1; w < NT / 64; ++w) {
     mx = sc.fmax[w] > mx ? sc.fmax[w] : mx;
     has_nan |= sc.fnan[w];
   }
   if (has_nan) mx = __builtin_nanf("");
   const float m = round_dt<DT>(mx + 1e-6f);
-  for (int i = tid; i < n; i += kSelThreads) {
+  for (int i = tid; i < n; i += NT) {
     const float s = round_dt<DT>(m - load_dt<DT>(nrow, i));
     if constexpr (DT == KVC_BF16)
       reinterpret_cast<uint16_t*>(tmp)[i] = (uint16_t)f32_to_bf16_rne(s);
@@ -325,7 +336,7 @@ __device__ void snapkv_keys(const char* nrow, int n, int pool_k, bool desc, KeyT
   __syncthreads();
   const bool pool = pool_k > 1 && n >= pool_k;
   const int pad = pool_k / 2;
-  for (int i = tid; i < n; i += kSelThreads) {
+  for (int i = tid; i < n; i += NT) {
     float r;
     if (pool) {
       int hs = i - pad;
@@ -398,7 +409,7 @@ __device__ __forceinline__ int mbcnt(uint64_t mask, int base) {
 template <typename KeyT, int NT, int JM>
 __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_t* spos,
                                                uint16_t* gpos, SelScalars<KeyT>& sc, int lo,
-                                               int hi, uint64_t* acc) {
+                                               int hi, int cap, uint64_t* acc) {
   constexpr int NW = NT / 64;
   typedef typename std::conditional<(JM > 32), uint64_t, uint32_t>::type MaskT;
   const int lane = threadIdx.x & 63;
@@ -464,72 +475,93 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
     tot_le = (int)((uint32_t)__builtin_amdgcn_readlane(scan, NW - 1) >> 16);
   }
   KVC_TICK(t1);
-  // ---- P2: s rank table, swap count m, g_{m+1} (stores only) ----
+  // ---- P2: s rank table, swap count m, g_{m+1} (stores only).  The tables hold the ranks
+  // (wb, wb + cap] of one window: window 0 also counts m; a level with m > cap re-scatters the
+  // next window from its flags (still in registers; the swapped pairs are disjoint, so earlier
+  // windows' swaps do not change them) after the previous window's swaps ----
   if (tid == 0) kv_swap(key, idx, lo, ch);  // the median move, made physical
-  int rge = ge_before, rle = le_before, nsw = 0, ff = kBig;
+  int msw = 0, gnext = kBig, wb = 0;
+  while (true) {
+    const bool count = wb == 0;
+    int rge = ge_before, rle = le_before, nsw = 0, ff = kBig;
 #pragma unroll
-  for (int j = 0; j < JM; ++j) {
-    if (j >= J) break;
-    const bool ge = (gem >> j) & 1, le = (lem >> j) & 1;
-    const uint64_t bg = __builtin_amdgcn_ballot_w64(ge), bl = __builtin_amdgcn_ballot_w64(le);
-    const int A = mbcnt(bg, rge);                 // ge positions before this one
-    const int lin = mbcnt(bl, rle) + (le ? 1 : 0);  // le positions in [lo+1, pos]
-    const bool cond = A + lin < tot_le;
-    const uint16_t pj = (uint16_t)(pos0 + j * 64);
-    spos[le ? tot_le - lin + 1 : lane - 64] = pj;
-    gpos[(ge && cond) ? A + 1 : lane - 64] = pj;  // swapped: rank A + 1 <= m
-    const uint64_t bc = __builtin_amdgcn_ballot_w64(cond);
-    nsw += __popcll(bg & bc);
-    const uint64_t bf = bg & ~bc;  // first unswapped ge: positions grow with j, so min = first
-    ff = min(ff, bf ? wbeg + j * 64 + (int)__builtin_ctzll(bf) : kBig);
-    rge += __popcll(bg);
-    rle += __popcll(bl);
-  }
-  int msw, gnext;
-  if constexpr (NW > 1) {
-    if (lane == 0)  // ff < 65535
-      sc.wm[wid] = (int)((uint32_t)nsw | ((uint32_t)(ff == kBig ? 0xFFFF : ff) << 16));
-    __syncthreads();  // B_b
-    const uint32_t x = lane < NW ? (uint32_t)sc.wm[lane] : 0xFFFF0000u;
-    msw = __builtin_amdgcn_readlane(row_scan16((int)(x & 0xFFFFu)), NW - 1);
-    const uint64_t fb = __builtin_amdgcn_ballot_w64((x >> 16) != 0xFFFFu);  // waves in position order: first wins
-    gnext = fb ? (int)((uint32_t)__builtin_amdgcn_readlane((int)x, (int)__builtin_ctzll(fb)) >> 16)
-               : kBig;
-  } else {
-    wave_sync();
-    msw = nsw;
-    gnext = ff;
-  }
-  KVC_TICK(t2);
-  // ---- P4: the m swaps (disjoint pairs g_t <-> s_t), spread evenly over the NT lanes:
-  // rank-table loads, then key/idx loads, then stores ----
-  for (int base = 1; base <= msw; base += NT * 4) {
-    if (base + wid * 64 > msw) break;  // no rank left for this wave
-    int gp[4], sp[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int t = base + tid + q * NT;
-      gp[q] = gpos[t <= msw ? t : 0];
-      sp[q] = spos[t <= msw ? t : 0];
+    for (int j = 0; j < JM; ++j) {
+      if (j >= J) break;
+      const bool ge = (gem >> j) & 1, le = (lem >> j) & 1;
+      const uint64_t bg = __builtin_amdgcn_ballot_w64(ge), bl = __builtin_amdgcn_ballot_w64(le);
+      const int A = mbcnt(bg, rge);                 // ge positions before this one
+      const int lin = mbcnt(bl, rle) + (le ? 1 : 0);  // le positions in [lo+1, pos]
+      const bool cond = A + lin < tot_le;
+      const uint16_t pj = (uint16_t)(pos0 + j * 64);
+      const int sr = tot_le - lin + 1 - wb;  // s rank within the window
+      spos[(le && sr >= 1 && sr <= cap) ? sr : lane - 64] = pj;
+      const int gr = A + 1 - wb;             // swapped (cond): g rank A + 1 <= m
+      gpos[(ge && cond && gr >= 1 && gr <= cap) ? gr : lane - 64] = pj;
+      if (count) {
+        const uint64_t bc = __builtin_amdgcn_ballot_w64(cond);
+        nsw += __popcll(bg & bc);
+        const uint64_t bf = bg & ~bc;  // first unswapped ge: positions grow with j, so min = first
+        ff = min(ff, bf ? wbeg + j * 64 + (int)__builtin_ctzll(bf) : kBig);
+      }
+      rge += __popcll(bg);
+      rle += __popcll(bl);
     }
-    KeyT kg[4], ks[4];
-    uint16_t ig[4], is[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      kg[q] = key[gp[q]];
-      ks[q] = key[sp[q]];
-      ig[q] = idx[gp[q]];
-      is[q] = idx[sp[q]];
+    if (count) {
+      if constexpr (NW > 1) {
+        if (lane == 0)  // ff < 65535
+          sc.wm[wid] = (int)((uint32_t)nsw | ((uint32_t)(ff == kBig ? 0xFFFF : ff) << 16));
+        __syncthreads();  // B_b
+        const uint32_t x = lane < NW ? (uint32_t)sc.wm[lane] : 0xFFFF0000u;
+        msw = __builtin_amdgcn_readlane(row_scan16((int)(x & 0xFFFFu)), NW - 1);
+        // waves in position order: the first one with an unswapped ge position wins
+        const uint64_t fb = __builtin_amdgcn_ballot_w64((x >> 16) != 0xFFFFu);
+        gnext = fb ? (int)((uint32_t)__builtin_amdgcn_readlane((int)x, (int)__builtin_ctzll(fb)) >> 16)
+                   : kBig;
+      } else {
+        wave_sync();
+        msw = nsw;
+        gnext = ff;
+      }
+      KVC_TICK(t2);
+    } else {
+      group_sync<NT>();
     }
+    // ---- P4: this window's swaps (disjoint pairs g_t <-> s_t), spread evenly over the NT
+    // lanes: rank-table loads, then key/idx loads, then stores ----
+    const int wend = min(msw, wb + cap);
+    for (int base = wb + 1; base <= wend; base += NT * 4) {
+      if (base + wid * 64 > wend) break;  // no rank left for this wave
+      int gp[4], sp[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (base + tid + q * NT <= msw) {
-        key[gp[q]] = ks[q];
-        key[sp[q]] = kg[q];
-        idx[gp[q]] = is[q];
-        idx[sp[q]] = ig[q];
+      for (int q = 0; q < 4; ++q) {
+        const int t = base + tid + q * NT;
+        const int ti = t <= wend ? t - wb : 0;
+        const int g = gpos[ti], sv = spos[ti];
+        gp[q] = t <= wend ? g : lo;
+        sp[q] = t <= wend ? sv : lo;
+      }
+      KeyT kg[4], ks[4];
+      uint16_t ig[4], is[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        kg[q] = key[gp[q]];
+        ks[q] = key[sp[q]];
+        ig[q] = idx[gp[q]];
+        is[q] = idx[sp[q]];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (base + tid + q * NT <= wend) {
+          key[gp[q]] = ks[q];
+          key[sp[q]] = kg[q];
+          idx[gp[q]] = is[q];
+          idx[sp[q]] = ig[q];
+        }
       }
     }
+    if (wend >= msw) break;
+    group_sync<NT>();  // the next window overwrites the tables
+    wb += cap;
   }
   group_sync<NT>();  // B_c
   KVC_TICK(t3);
@@ -543,7 +575,7 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
     if (NT > 64) acc[25] = (t1 - t0) | ((t2 - t1) << 20) | ((t3 - t2) << 40);  // level split
   }
 #endif
-  return min(gnext, msw > 0 ? uni((int)spos[msw]) : kBig);
+  return min(gnext, msw > 0 ? uni((int)spos[msw - wb]) : kBig);
 }
 
 // The partition chain of libstdc++ introsort (topk = false) / introselect (topk = true),
@@ -563,8 +595,9 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
 // Returns 0 when the first-k set is final, 1 when the block hands a short segment to one wave.
 template <typename KeyT, int NT, int MAXJ>
 __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, uint16_t* gpos,
-                         SelScalars<KeyT>& sc, int k, bool topk, int thr, int& lo, int& hi,
-                         int& depth, int& level, int wave_seg, uint64_t* acc = nullptr) {
+                         SelScalars<KeyT>& sc, int k, bool topk, int thr, int cap, int& lo,
+                         int& hi, int& depth, int& level, int wave_seg,
+                         uint64_t* acc = nullptr) {
   const int tid = (NT == 64) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   while (true) {
     if (lo == k || hi == k) return 0;  // a partition boundary sits at k: the set is final
@@ -594,20 +627,20 @@ __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, uint16_t* gpo
     const uint64_t tl0 = __builtin_amdgcn_s_memtime();
 #endif
     if (J <= 1)
-      cut = partition_level<KeyT, NT, 1>(key, idx, spos, gpos, sc, lo, hi, acc);
+      cut = partition_level<KeyT, NT, 1>(key, idx, spos, gpos, sc, lo, hi, cap, acc);
     else if (J <= 2)
-      cut = partition_level<KeyT, NT, 2>(key, idx, spos, gpos, sc, lo, hi, acc);
+      cut = partition_level<KeyT, NT, 2>(key, idx, spos, gpos, sc, lo, hi, cap, acc);
     else if (J <= 4)
-      cut = partition_level<KeyT, NT, 4>(key, idx, spos, gpos, sc, lo, hi, acc);
+      cut = partition_level<KeyT, NT, 4>(key, idx, spos, gpos, sc, lo, hi, cap, acc);
     else if (J <= 8)
-      cut = partition_level<KeyT, NT, 8>(key, idx, spos, gpos, sc, lo, hi, acc);
+      cut = partition_level<KeyT, NT, 8>(key, idx, spos, gpos, sc, lo, hi, cap, acc);
     else if (MAXJ <= 16 || J <= 16)
-      cut = partition_level<KeyT, NT, 16>(key, idx, spos, gpos, sc, lo, hi, acc);
+      cut = partition_level<KeyT, NT, 16>(key, idx, spos, gpos, sc, lo, hi, cap, acc);
     else if (J <= 32)
-      cut = partition_level<KeyT, NT, (MAXJ < 32 ? 16 : 32)>(key, idx, spos, gpos, sc, lo, hi,
+      cut = partition_level<KeyT, NT, (MAXJ < 32 ? 16 : 32)>(key, idx, spos, gpos, sc, lo, hi, cap,
                                                                acc);
     else
-      cut = partition_level<KeyT, NT, (MAXJ < 64 ? 16 : 64)>(key, idx, spos, gpos, sc, lo, hi,
+      cut = partition_level<KeyT, NT, (MAXJ < 64 ? 16 : 64)>(key, idx, spos, gpos, sc, lo, hi, cap,
                                                                acc);
 #ifdef KVC_STAMPS
     // per block level (first 8): cycles, and segment length  (slots 16.. of the row)
@@ -626,20 +659,20 @@ __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, uint16_t* gpo
 }
 
 // Reference-exact selection for one (layer, b, h) row whose zone norms are at `nrow`; working
-// arrays at `arrays` (SelArrays layout for n_cap positions: LDS, or a global scratch row for
-// zones longer than kZoneMax) and scalars in `sc`.  Emits the kept zone-local indices in
-// ascending order to `out` (global int32) or, with TO_LDS, to `sel` (LDS u16, may alias
-// the key region: keys are dead by then).
-template <int DT, bool TO_LDS, int MAXN>
+// arrays at `arrays` (SelArrays layout for n_cap positions and `cap`-rank windows: LDS, or a
+// global scratch row for zones longer than kZoneMax) and scalars in `sc`; NT threads (the
+// workgroup) cooperate.  Emits the kept zone-local indices in ascending order to `out` (global
+// int32) or, with TO_LDS, to `sel` (LDS u16, may alias the key region: keys are dead by then).
+template <int DT, bool TO_LDS, int MAXN, int NT>
 __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, int order, int algo,
                             const char* __restrict__ nrow, int32_t* out, uint16_t* sel,
-                            char* arrays, int n_cap,
+                            char* arrays, int n_cap, int cap,
                             SelScalars<typename DTypeTraits<DT>::key_t>& sc,
                             int wave_seg, uint64_t* stamps) {
   typedef typename DTypeTraits<DT>::key_t KeyT;
   constexpr int ESZ = DTypeTraits<DT>::esz;
-  constexpr int MAXJ = (MAXN + kSelThreads - 1) / kSelThreads;  // positions per lane, level 0
-  const SelArrays<KeyT> A(arrays, n_cap);
+  constexpr int MAXJ = (MAXN + NT - 1) / NT;  // positions per lane, level 0
+  const SelArrays<KeyT> A(arrays, n_cap, cap);
   KeyT* key = A.key;
   uint16_t* idx = A.idx;
   uint16_t* spos = A.spos;
@@ -649,7 +682,7 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
   if (k <= 0 || n <= 0 || n > MAXN || n > n_cap) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (k >= n) {  // keep everything (e.g. h2o_l2 when the middle is no longer than heavy_hitter)
-    for (int i = tid; i < n; i += kSelThreads) {
+    for (int i = tid; i < n; i += NT) {
       if constexpr (TO_LDS) sel[i] = (uint16_t)i;
       else out[i] = i;
     }
@@ -659,27 +692,28 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
 
   // ---- keys ----
   if (ly->score_mode == KVC_SCORE_SNAPKV) {
-    // scratch for the unpooled scores: bf16 -> spos region, fp32 -> idx+spos (64 KiB + 16 B)
-    char* tmp = (DT == KVC_BF16) ? reinterpret_cast<char*>(spos) : reinterpret_cast<char*>(idx);
-    snapkv_keys<DT, KeyT>(nrow, n, ly->pool_kernel, desc, key, tmp, sc);
+    // scratch for the unpooled scores from the idx region on: n u16 (bf16), or n floats over
+    // idx + the rank tables (fp32 rows always get full n/2-rank tables: >= 4n bytes)
+    char* tmp = reinterpret_cast<char*>(idx);
+    snapkv_keys<DT, KeyT, NT>(nrow, n, ly->pool_kernel, desc, key, tmp, sc);
     __syncthreads();
-    for (int i = tid; i < n; i += kSelThreads) idx[i] = (uint16_t)i;
+    for (int i = tid; i < n; i += NT) idx[i] = (uint16_t)i;
   } else {
     // 16-B loads, all issued before the first use (norm rows are padded to 64 elements, so a
     // whole vector past n stays inside the row); keys/indices written as 16-B LDS stores
     constexpr int VEC = 16 / ESZ;
-    constexpr int MAXV = (kZoneMax / VEC + kSelThreads - 1) / kSelThreads;  // per batch
+    constexpr int MAXV = ((MAXN < kZoneMax ? MAXN : kZoneMax) / VEC + NT - 1) / NT;  // per batch
     const int nvec = (n + VEC - 1) / VEC;
-    for (int v0 = 0; v0 < nvec; v0 += MAXV * kSelThreads) {  // one batch for n <= kZoneMax
+    for (int v0 = 0; v0 < nvec; v0 += MAXV * NT) {  // one batch for n <= kZoneMax
     uint4 buf[MAXV];
 #pragma unroll
     for (int q = 0; q < MAXV; ++q) {
-      const int v = v0 + tid + q * kSelThreads;
+      const int v = v0 + tid + q * NT;
       if (v < nvec) buf[q] = reinterpret_cast<const uint4*>(nrow)[v];
     }
 #pragma unroll
     for (int q = 0; q < MAXV; ++q) {
-      const int v = v0 + tid + q * kSelThreads;
+      const int v = v0 + tid + q * NT;
       if (v < nvec) {
         const uint32_t w[4] = {buf[q].x, buf[q].y, buf[q].z, buf[q].w};
         uint32_t kw[4], iw[4];
@@ -725,23 +759,24 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
         for (int q = 0; q < 27; ++q) accb[q] = 0;
     }
 #endif
-    const int st = run_chain<KeyT, kSelThreads, MAXJ>(key, idx, spos, A.gpos, sc, k, topk, thr,
-                                                      lo, hi, depth, level, wave_seg, accb);
+    const int st = run_chain<KeyT, NT, MAXJ>(key, idx, spos, A.gpos, sc, k, topk, thr, cap, lo,
+                                             hi, depth, level, wave_seg, accb);
     KVC_STAMP(2);
     if (st == 1 && wid == 0)
-      run_chain<KeyT, 64, 16>(key, idx, spos, A.gpos, sc, k, topk, thr, lo, hi, depth, level,
-                              wave_seg, accw);
+      run_chain<KeyT, 64, 16>(key, idx, spos, A.gpos, sc, k, topk, thr, cap, lo, hi, depth,
+                              level, wave_seg, accw);
   }
   __syncthreads();
   KVC_STAMP(3);
 
-  // ---- emit the kept set {idx[0..k)} as ascending zone-local indices ----
-  uint16_t* flag = spos;
-  for (int i = tid; i < n; i += kSelThreads) flag[i] = 0;
+  // ---- emit the kept set {idx[0..k)} as ascending zone-local indices (flags in the key
+  // region: the keys are dead, and every flag is read into registers before `sel` is written)
+  uint16_t* flag = reinterpret_cast<uint16_t*>(key);
+  for (int i = tid; i < n; i += NT) flag[i] = 0;
   __syncthreads();
-  for (int i = tid; i < k; i += kSelThreads) flag[idx[i]] = 1;
+  for (int i = tid; i < k; i += NT) flag[idx[i]] = 1;
   __syncthreads();
-  const int J = (n + kSelThreads - 1) / kSelThreads;
+  const int J = (n + NT - 1) / NT;
   const int wbeg = wid * J * 64;
   uint64_t fm = 0;  // J <= 64
   int c = 0;
@@ -769,21 +804,24 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
 }
 
 
-template <int DT>
-__global__ void __launch_bounds__(kSelThreads)
+// One workgroup of NT threads per (layer, b, h) row, arrays in dynamic LDS sized by the call's
+// longest zone (n_cap): NT = 256 for zones up to 4 096 positions (several rows per CU), 1 024
+// beyond (two rows per CU for bf16 thanks to the rank windows).
+template <int DT, int NT>
+__global__ void __launch_bounds__(NT, 8)  // 8 waves per SIMD: two 1024-thread rows per CU
     select_kernel(const LayerChunk T, int BH, int order, int algo,
                   const char* __restrict__ norms, int64_t norm_stride,
-                  int32_t* __restrict__ out_idx, int64_t idx_stride, int wave_seg,
-                  uint64_t* stamps) {
-  typedef typename DTypeTraits<DT>::key_t KeyT;
+                  int32_t* __restrict__ out_idx, int64_t idx_stride, int wave_seg, int n_cap,
+                  int cap, uint64_t* stamps) {
   constexpr int ESZ = DTypeTraits<DT>::esz;
-  // LDS: key[kZoneMax] | idx[kZoneMax] (u16) | spos[kSposLen] | gpos[kGposLen] (u16) | scalars
-  __shared__ __attribute__((aligned(16))) char smem[kSelLdsBytes<KeyT>];
-  __shared__ SelScalars<KeyT> sc;
+  constexpr int MAXN = NT == 1024 ? kZoneMax : NT * 16;
+  // LDS: key[n_cap] | idx[n_cap] (u16) | spos | gpos (u16 rank windows) -- SelArrays
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ SelScalars<typename DTypeTraits<DT>::key_t> sc;
   const kvc_layer_t* ly = T.l + blockIdx.x / BH;
   const int row = ly->row0 + (int)(blockIdx.x % BH);  // global workspace row
-  select_body<DT, false, kZoneMax>(ly, order, algo, norms + (int64_t)row * norm_stride * ESZ,
-                                   out_idx + (int64_t)row * idx_stride, nullptr, smem, kZoneMax,
+  select_body<DT, false, MAXN, NT>(ly, order, algo, norms + (int64_t)row * norm_stride * ESZ,
+                                   out_idx + (int64_t)row * idx_stride, nullptr, smem, n_cap, cap,
                                    sc, wave_seg, stamps);
 }
 
@@ -801,11 +839,10 @@ __global__ void __launch_bounds__(kSelThreads)
   __shared__ SelScalars<KeyT> sc;
   const kvc_layer_t* ly = T.l + blockIdx.x / BH;
   const int row = ly->row0 + (int)(blockIdx.x % BH);
-  select_body<DT, false, kZoneMaxGlobal>(ly, order, algo,
-                                         norms + (int64_t)row * norm_stride * ESZ,
-                                         out_idx + (int64_t)row * idx_stride, nullptr,
-                                         scratch + (int64_t)row * scratch_row_bytes, n_cap, sc,
-                                         wave_seg, nullptr);
+  select_body<DT, false, kZoneMaxGlobal, kSelThreads>(
+      ly, order, algo, norms + (int64_t)row * norm_stride * ESZ,
+      out_idx + (int64_t)row * idx_stride, nullptr, scratch + (int64_t)row * scratch_row_bytes,
+      n_cap, n_cap / 2 + 1, sc, wave_seg, nullptr);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1005,7 +1042,7 @@ __global__ void __launch_bounds__(kSelThreads)
   static_assert(NC == 8 || NC == 16, "fused path: 128/256-byte rows");
   constexpr int ROWB = 8 * 16 + 16;
   constexpr int SCORE_B = kSelWaves * kTile * ROWB;
-  constexpr int SEL_B = kSelLdsBytes<KeyT>;
+  constexpr int SEL_B = (int)sel_bytes(kZoneMax, (int)sizeof(KeyT), kZoneMax / 2 + 1);
   constexpr int SM_B = SCORE_B > SEL_B ? SCORE_B : SEL_B;
   __shared__ __attribute__((aligned(16))) char smem[SM_B];
   __shared__ SelScalars<KeyT> sc;
@@ -1081,8 +1118,10 @@ __global__ void __launch_bounds__(kSelThreads)
       __syncthreads();
       KVC_TL(r * 4 + 1);
       uint16_t* sel = reinterpret_cast<uint16_t*>(smem);  // key region, dead after the chain
-      select_body<DT, true, kZoneMax>(ly, order, algo, norms + (int64_t)r * norm_stride * ESZ,
-                                      nullptr, sel, smem, kZoneMax, sc, wave_seg, nullptr);
+      select_body<DT, true, kZoneMax, kSelThreads>(ly, order, algo,
+                                                   norms + (int64_t)r * norm_stride * ESZ, nullptr,
+                                                   sel, smem, kZoneMax, kZoneMax / 2 + 1, sc,
+                                                   wave_seg, nullptr);
       __syncthreads();
       KVC_TL(r * 4 + 2);
       gather_row<DT, NC>(ly, row, H, sel);
@@ -1105,7 +1144,7 @@ static inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; 
 static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 // one row of the global selection scratch (SelArrays for n_cap positions), 256-B aligned rows
 static inline size_t sel_scratch_row_bytes(int n_cap, int dtype) {
-  return round_up(sel_bytes(n_cap, dtype == KVC_BF16 ? 2 : 4), 256);
+  return round_up(sel_bytes(n_cap, dtype == KVC_BF16 ? 2 : 4, n_cap / 2 + 1), 256);
 }
 
 static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_plan_info_t* info,
@@ -1380,14 +1419,33 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
                            p->algo, norms, info.norm_row_stride, idx, info.index_row_stride,
                            wave_seg, scratch, rb, n_cap);
     } else if ((p->phases & KVC_PHASE_SELECT) && sel && !p->external_index) {
-      const dim3 grid((unsigned)(cn * BH)), block(kSelThreads);
       uint64_t* st = stamps ? stamps + (size_t)layers[c0].row0 * 32 : nullptr;
-      if (p->dtype == KVC_BF16)
-        hipLaunchKernelGGL(select_kernel<KVC_BF16>, grid, block, 0, s, T, BH, p->order, p->algo,
-                           norms, info.norm_row_stride, idx, info.index_row_stride, wave_seg, st);
-      else
-        hipLaunchKernelGGL(select_kernel<KVC_F32>, grid, block, 0, s, T, BH, p->order, p->algo,
-                           norms, info.norm_row_stride, idx, info.index_row_stride, wave_seg, st);
+      const int n_cap = (int)info.norm_row_stride;  // longest zone of the call, rounded to 64
+      const int ks = p->dtype == KVC_BF16 ? 2 : 4;
+      const int cap = sel_cap(n_cap, ks);
+      const size_t lds = sel_bytes(n_cap, ks, cap);
+      const dim3 grid((unsigned)(cn * BH));
+      rc = KVC_OK;
+#define KVC_SEL_LAUNCH(DT_, NT_)                                                                \
+  do {                                                                                         \
+    if (lds > 65536 && hipFuncSetAttribute((const void*)select_kernel<DT_, NT_>,               \
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,         \
+                                           (int)lds) != hipSuccess)                            \
+      rc = KVC_E_HIP;                                                                          \
+    else                                                                                       \
+      hipLaunchKernelGGL((select_kernel<DT_, NT_>), grid, dim3(NT_), lds, s, T, BH, p->order,  \
+                         p->algo, norms, info.norm_row_stride, idx, info.index_row_stride,     \
+                         wave_seg, n_cap, cap, st);                                            \
+  } while (0)
+      if (p->dtype == KVC_BF16) {
+        if (n_cap <= kSmallZone) KVC_SEL_LAUNCH(KVC_BF16, kSelThreadsSmall);
+        else KVC_SEL_LAUNCH(KVC_BF16, kSelThreads);
+      } else {
+        if (n_cap <= kSmallZone) KVC_SEL_LAUNCH(KVC_F32, kSelThreadsSmall);
+        else KVC_SEL_LAUNCH(KVC_F32, kSelThreads);
+      }
+#undef KVC_SEL_LAUNCH
+      if (rc != KVC_OK) return rc;
     }
     if ((p->phases & KVC_PHASE_GATHER) && max_out > 0) {
       if (p->dtype == KVC_BF16)

@@ -51,3 +51,11 @@ if [ "$MODE" = "pmc" ]; then
   done
   find "$R/gpurun_out" -name "*counter_collection*" | head
 fi
+if [ "$MODE" = "workloads" ]; then  # every bench.py workload at N=1 (and strong-scaled cfg4 shape)
+  : > gpurun_out/workloads.jsonl
+  for w in ${2:-fix512-s16384 fix512-s4096 fix512-s4096-d80 streaming-s16384 h2o-s16384 snapkv-s16384 pyramid-s16384 l2-s16384 adaptive-s16384}; do
+    timeout -k 10 200 python bench.py --workload $w --steps 20 --warmup 5 ${3:---no-cpu-baseline} \
+        >> gpurun_out/workloads.jsonl 2>> gpurun_out/workloads.err || exit $?
+  done
+  cat gpurun_out/workloads.jsonl
+fi
