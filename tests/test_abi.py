@@ -99,7 +99,8 @@ def test_plan_long_zone_gets_global_scratch():
     rc1, i1 = N.plan(_params(), long_)
     assert rc0 == 0 and rc1 == 0
     n_cap = 40000 + (-40000 % 64)
-    row = n_cap * 2 + n_cap * 2 + (64 + n_cap + 8) * 2 + (64 + n_cap // 2 + 8) * 2
+    # key | idx | two rank tables of n_cap/2 + 1 ranks (+ 64 sinks + 8 pad each)
+    row = n_cap * 2 + n_cap * 2 + 2 * (64 + n_cap // 2 + 1 + 8) * 2
     row += -row % 256
     idx_end = i1.index_offset + 32 * i1.index_row_stride * 4
     idx_end += -idx_end % 256
