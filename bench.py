@@ -67,7 +67,8 @@ def job_bytes(jobs, es):
       path   = R * (zone + sink + tail + 3*out)   K scored over the zone, K rows copied from the
                sink/tail, V kept rows read, K and V out written (selected K rows not re-counted)
       score  = B*H*zone*(D*e + e)                 K read + one norm written per scored position
-      gather = 4 * R * out                        K,V kept rows read + written
+      select+gather = 4 * R * out                 K,V kept rows read + written (the selection's
+                                                  norm reads / index traffic stay on chip)
     """
     path = score = gather = 0
     for j in jobs:
@@ -78,7 +79,7 @@ def job_bytes(jobs, es):
         path += R * (zone + j.sink_len + j.tail_len + 3 * out)
         score += b * h * zone * (d * es + es)
         gather += 4 * R * out
-    return {"path": path, "score": score, "gather": gather}
+    return {"path": path, "score": score, "select+gather": gather}
 
 
 PMC_FILE = "profiles/r01_v7_pmc_traffic.json"  # tools/gpu_check.sh pmc + tools/pmc_traffic.py
@@ -242,8 +243,8 @@ def main():
         headline = args.workload == HEADLINE
         traffic = pmc_traffic() if headline and kern == "score" else None
         path_gbps = nbytes["path"] * world / (ms_step * 1e-3) / 1e9
-        desc = {"score": "score_kernel (key L2 norms)", "select": "select_kernel",
-                "gather": "gather_kernel (segment copy)"}[kern]
+        desc = {"score": "score_kernel (key L2 norms)",
+                "select+gather": "select_gather_kernel (selection + segment copy)"}[kern]
         cfg_kw = ", ".join(f"{k}={v!r}" for k, v in kwargs.items())
         res = {
             "metric": "KV tokens scored+evicted/sec at S=16384, fix_size=512; PPL delta vs ref",

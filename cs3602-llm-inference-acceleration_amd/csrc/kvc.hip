@@ -804,25 +804,39 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
 }
 
 
-// One workgroup of NT threads per (layer, b, h) row, arrays in dynamic LDS sized by the call's
-// longest zone (n_cap): NT = 256 for zones up to 4 096 positions (several rows per CU), 1 024
-// beyond (two rows per CU for bf16 thanks to the rank windows).
+// One workgroup of NT threads per (layer, b, h) row.  NT = 256 for zones up to 4 096
+// positions, arrays in dynamic LDS sized by the call's longest zone (n_cap): several rows per
+// CU.  NT = 1 024 beyond, arrays in static LDS laid out for kZoneMax (compile-time addresses)
+// with rank windows of kSelCapBig: two rows per CU for bf16.
+template <typename KeyT>
+constexpr int kSelCapBig = sel_cap(kZoneMax, (int)sizeof(KeyT));
+template <typename KeyT>
+constexpr int kSelBytesBig = (int)sel_bytes(kZoneMax, (int)sizeof(KeyT), kSelCapBig<KeyT>);
+
 template <int DT, int NT>
 __global__ void __launch_bounds__(NT, 8)  // 8 waves per SIMD: two 1024-thread rows per CU
     select_kernel(const LayerChunk T, int BH, int order, int algo,
                   const char* __restrict__ norms, int64_t norm_stride,
                   int32_t* __restrict__ out_idx, int64_t idx_stride, int wave_seg, int n_cap,
                   int cap, uint64_t* stamps) {
+  typedef typename DTypeTraits<DT>::key_t KeyT;
   constexpr int ESZ = DTypeTraits<DT>::esz;
-  constexpr int MAXN = NT == 1024 ? kZoneMax : NT * 16;
-  // LDS: key[n_cap] | idx[n_cap] (u16) | spos | gpos (u16 rank windows) -- SelArrays
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ SelScalars<typename DTypeTraits<DT>::key_t> sc;
+  constexpr int MAXN = NT == kSelThreads ? kZoneMax : NT * 16;
+  __shared__ SelScalars<KeyT> sc;
   const kvc_layer_t* ly = T.l + blockIdx.x / BH;
   const int row = ly->row0 + (int)(blockIdx.x % BH);  // global workspace row
-  select_body<DT, false, MAXN, NT>(ly, order, algo, norms + (int64_t)row * norm_stride * ESZ,
-                                   out_idx + (int64_t)row * idx_stride, nullptr, smem, n_cap, cap,
-                                   sc, wave_seg, stamps);
+  if constexpr (NT == kSelThreads) {
+    // LDS: key[kZoneMax] | idx[kZoneMax] (u16) | spos | gpos (u16 rank windows) -- SelArrays
+    __shared__ __attribute__((aligned(16))) char smem[kSelBytesBig<KeyT>];
+    select_body<DT, false, MAXN, NT>(ly, order, algo, norms + (int64_t)row * norm_stride * ESZ,
+                                     out_idx + (int64_t)row * idx_stride, nullptr, smem, kZoneMax,
+                                     kSelCapBig<KeyT>, sc, wave_seg, stamps);
+  } else {
+    extern __shared__ __attribute__((aligned(16))) char dsmem[];
+    select_body<DT, false, MAXN, NT>(ly, order, algo, norms + (int64_t)row * norm_stride * ESZ,
+                                     out_idx + (int64_t)row * idx_stride, nullptr, dsmem, n_cap,
+                                     cap, sc, wave_seg, stamps);
+  }
 }
 
 // Zones longer than kZoneMax (up to kZoneMaxGlobal): the same selection with its arrays in a
@@ -970,7 +984,7 @@ __device__ __forceinline__ const kvc_layer_t* tile_layer(const kvc_layer_t* L, i
 
 // Copy one output row (sink ++ selected ++ tail) of K and V with the whole workgroup.
 // sel: ascending zone-local kept indices in LDS, or nullptr when no selection ran.
-template <int DT, int NC>
+template <int DT, int NC, int NT = kSelThreads, bool NTS = false>
 __device__ __forceinline__ void gather_row(const kvc_layer_t* __restrict__ ly, int r, int H,
                                            const uint16_t* sel) {
   constexpr int ESZ = DTypeTraits<DT>::esz;
@@ -987,12 +1001,12 @@ __device__ __forceinline__ void gather_row(const kvc_layer_t* __restrict__ ly, i
   char* ko = static_cast<char*>(ly->k_out) + (int64_t)r * nu * 16;
   char* vo = static_cast<char*>(ly->v_out) + (int64_t)r * nu * 16;
   const int tid0 = opaque_tid();
-  for (int u0 = 0; u0 < nu; u0 += kSelThreads * BATCH) {
+  for (int u0 = 0; u0 < nu; u0 += NT * BATCH) {
     uint4 xk[BATCH], xv[BATCH];
     bool gat[BATCH];
 #pragma unroll
     for (int i = 0; i < BATCH; ++i) {
-      const int u = u0 + tid0 + i * kSelThreads;
+      const int u = u0 + tid0 + i * NT;
       gat[i] = false;
       if (u < nu) {
         const int t = u / NC, c = u - (u / NC) * NC;
@@ -1013,7 +1027,7 @@ __device__ __forceinline__ void gather_row(const kvc_layer_t* __restrict__ ly, i
     }
 #pragma unroll
     for (int i = 0; i < BATCH; ++i) {
-      const int u = u0 + tid0 + i * kSelThreads;
+      const int u = u0 + tid0 + i * NT;
       if (u < nu) {
         uint4 a = xk[i], q = xv[i];
         if constexpr (DT == KVC_BF16) {
@@ -1024,8 +1038,16 @@ __device__ __forceinline__ void gather_row(const kvc_layer_t* __restrict__ ly, i
             q.z = canon_nan_bf16x2(q.z); q.w = canon_nan_bf16x2(q.w);
           }
         }
-        *reinterpret_cast<uint4*>(ko + (int64_t)u * 16) = a;
-        *reinterpret_cast<uint4*>(vo + (int64_t)u * 16) = q;
+        if constexpr (NTS) {  // written once: non-temporal
+          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+          __builtin_nontemporal_store(u32x4{a.x, a.y, a.z, a.w},
+                                      reinterpret_cast<u32x4*>(ko + (int64_t)u * 16));
+          __builtin_nontemporal_store(u32x4{q.x, q.y, q.z, q.w},
+                                      reinterpret_cast<u32x4*>(vo + (int64_t)u * 16));
+        } else {
+          *reinterpret_cast<uint4*>(ko + (int64_t)u * 16) = a;
+          *reinterpret_cast<uint4*>(vo + (int64_t)u * 16) = q;
+        }
       }
     }
   }
@@ -1134,6 +1156,46 @@ __global__ void __launch_bounds__(kSelThreads)
     r = __builtin_amdgcn_readfirstlane(sh_val);
     __syncthreads();
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// SELECT + GATHER: one workgroup per (layer, b, h) row selects into LDS and copies the row's
+// output (sink ++ selected ++ tail of K and V) straight from the LDS index list.  With two
+// workgroups per CU, one row's copy (HBM-bound) overlaps the other's selection (LDS/issue-
+// bound), and the index list never round-trips through global memory.  Layout and thread
+// counts as select_kernel; rows without a selection only copy.
+// ---------------------------------------------------------------------------------------------
+template <int DT, int NT, int NC>
+__global__ void __launch_bounds__(NT, 8)
+    select_gather_kernel(const LayerChunk T, int H, int BH, int order, int algo,
+                         const char* __restrict__ norms, int64_t norm_stride, int wave_seg,
+                         int n_cap, int cap) {
+  typedef typename DTypeTraits<DT>::key_t KeyT;
+  constexpr int ESZ = DTypeTraits<DT>::esz;
+  constexpr int MAXN = NT == kSelThreads ? kZoneMax : NT * 16;
+  __shared__ SelScalars<KeyT> sc;
+  const kvc_layer_t* ly = T.l + blockIdx.x / BH;
+  const int r = (int)(blockIdx.x % BH);
+  if (ly->n_out == 0) return;
+  const bool selects = fused_selects(*ly);
+  const char* nrow = norms + (int64_t)(ly->row0 + r) * norm_stride * ESZ;
+  char* arrays;
+  if constexpr (NT == kSelThreads) {
+    __shared__ __attribute__((aligned(16))) char smem[kSelBytesBig<KeyT>];
+    arrays = smem;
+    n_cap = kZoneMax;
+    cap = kSelCapBig<KeyT>;
+  } else {
+    extern __shared__ __attribute__((aligned(16))) char dsmem[];
+    arrays = dsmem;
+  }
+  uint16_t* sel = reinterpret_cast<uint16_t*>(arrays);  // key region, dead after the chain
+  if (selects) {
+    select_body<DT, true, MAXN, NT>(ly, order, algo, nrow, nullptr, sel, arrays, n_cap, cap, sc,
+                                    wave_seg, nullptr);
+    __syncthreads();
+  }
+  gather_row<DT, NC, NT, true>(ly, r, H, selects ? sel : nullptr);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1275,6 +1337,28 @@ static void dispatch_nc(int nc, bool score, const LayerChunk& T, int nl, int H, 
       break;
   }
 #undef KVC_NC_CASE
+}
+
+template <int DT, int NT>
+static void launch_select_gather(int nc, const LayerChunk& T, int nl, int H, int BH, int order,
+                                 int algo, const char* norms, int64_t nstride, int wave_seg,
+                                 int n_cap, int cap, size_t lds, hipStream_t s) {
+  const dim3 grid((unsigned)(nl * BH));
+#define KVC_SG_CASE(NCV)                                                                    \
+  case NCV:                                                                                 \
+    hipLaunchKernelGGL((select_gather_kernel<DT, NT, NCV>), grid, dim3(NT), lds, s, T, H, BH, \
+                       order, algo, norms, nstride, wave_seg, n_cap, cap);                  \
+    break;
+  switch (nc) {
+    KVC_SG_CASE(8)
+    KVC_SG_CASE(10)
+    KVC_SG_CASE(16)
+    KVC_SG_CASE(20)
+    KVC_SG_CASE(32)
+    default:
+      break;
+  }
+#undef KVC_SG_CASE
 }
 
 }  // namespace kvc
@@ -1422,30 +1506,39 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
       uint64_t* st = stamps ? stamps + (size_t)layers[c0].row0 * 32 : nullptr;
       const int n_cap = (int)info.norm_row_stride;  // longest zone of the call, rounded to 64
       const int ks = p->dtype == KVC_BF16 ? 2 : 4;
-      const int cap = sel_cap(n_cap, ks);
-      const size_t lds = sel_bytes(n_cap, ks, cap);
+      const char* ent = getenv("KVC_SEL_NT");  // tuning only: 1024 = no small variant
+      const bool small = n_cap <= kSmallZone && !(ent && atoi(ent) == 1024);
+      const int cap = small ? sel_cap(n_cap, ks) : 0;
+      const size_t lds = small ? sel_bytes(n_cap, ks, cap) : 0;
+      // SELECT + GATHER in one kernel when both phases run (KVC_SEL_GATHER=0: separate kernels)
+      const char* esg = getenv("KVC_SEL_GATHER");
+      const bool fuse_sg = (p->phases & KVC_PHASE_GATHER) && max_out > 0 && !stamps &&
+                           !(esg && strcmp(esg, "0") == 0);
+      if (fuse_sg) {
+#define KVC_SG(DT_, NT_)                                                                      \
+  launch_select_gather<DT_, NT_>(nc, T, cn, H, BH, p->order, p->algo, norms,                   \
+                                 info.norm_row_stride, wave_seg, n_cap, cap, lds, s)
+        if (p->dtype == KVC_BF16) {
+          if (small) KVC_SG(KVC_BF16, kSelThreadsSmall); else KVC_SG(KVC_BF16, kSelThreads);
+        } else {
+          if (small) KVC_SG(KVC_F32, kSelThreadsSmall); else KVC_SG(KVC_F32, kSelThreads);
+        }
+#undef KVC_SG
+        continue;  // this chunk's gather is done
+      }
       const dim3 grid((unsigned)(cn * BH));
-      rc = KVC_OK;
-#define KVC_SEL_LAUNCH(DT_, NT_)                                                                \
-  do {                                                                                         \
-    if (lds > 65536 && hipFuncSetAttribute((const void*)select_kernel<DT_, NT_>,               \
-                                           hipFuncAttributeMaxDynamicSharedMemorySize,         \
-                                           (int)lds) != hipSuccess)                            \
-      rc = KVC_E_HIP;                                                                          \
-    else                                                                                       \
-      hipLaunchKernelGGL((select_kernel<DT_, NT_>), grid, dim3(NT_), lds, s, T, BH, p->order,  \
-                         p->algo, norms, info.norm_row_stride, idx, info.index_row_stride,     \
-                         wave_seg, n_cap, cap, st);                                            \
-  } while (0)
+#define KVC_SEL_LAUNCH(DT_, NT_)                                                              \
+  hipLaunchKernelGGL((select_kernel<DT_, NT_>), grid, dim3(NT_), lds, s, T, BH, p->order,    \
+                     p->algo, norms, info.norm_row_stride, idx, info.index_row_stride,       \
+                     wave_seg, n_cap, cap, st)
       if (p->dtype == KVC_BF16) {
-        if (n_cap <= kSmallZone) KVC_SEL_LAUNCH(KVC_BF16, kSelThreadsSmall);
+        if (small) KVC_SEL_LAUNCH(KVC_BF16, kSelThreadsSmall);
         else KVC_SEL_LAUNCH(KVC_BF16, kSelThreads);
       } else {
-        if (n_cap <= kSmallZone) KVC_SEL_LAUNCH(KVC_F32, kSelThreadsSmall);
+        if (small) KVC_SEL_LAUNCH(KVC_F32, kSelThreadsSmall);
         else KVC_SEL_LAUNCH(KVC_F32, kSelThreads);
       }
 #undef KVC_SEL_LAUNCH
-      if (rc != KVC_OK) return rc;
     }
     if ((p->phases & KVC_PHASE_GATHER) && max_out > 0) {
       if (p->dtype == KVC_BF16)

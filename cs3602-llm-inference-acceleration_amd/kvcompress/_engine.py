@@ -44,12 +44,17 @@ _SUPPORTED = {torch.bfloat16: N.KVC_BF16, torch.float32: N.KVC_F32}
 class PhaseTimer:
     """When installed with set_phase_timer(), every engine launch is bracketed by HIP events
     (torch.cuda.Event, recorded on the stream the kernels run on) so kernel durations can be
-    measured live (bench.py).  split=True additionally launches the SCORE / SELECT / GATHER
-    phases separately (three-kernel path) and times each; split=False times the launch as
-    issued ("all": the fused persistent kernel when it applies)."""
+    measured live (bench.py).  split=True launches the phases of `steps` separately and times
+    each: by default SCORE, then SELECT+GATHER (one select_gather kernel, as in an untimed
+    call); THREE times SCORE / SELECT / GATHER as separate kernels.  split=False times the
+    launch as issued ("all")."""
 
-    def __init__(self, split=True, keep_workspace=False):
+    DEFAULT = (("score", N.PHASE_SCORE), ("select+gather", N.PHASE_SELECT | N.PHASE_GATHER))
+    THREE = (("score", N.PHASE_SCORE), ("select", N.PHASE_SELECT), ("gather", N.PHASE_GATHER))
+
+    def __init__(self, split=True, keep_workspace=False, steps=None):
         self.split = split
+        self.steps = steps or self.DEFAULT
         self.records = []
         self.workspaces = [] if keep_workspace else None  # (ws, info) of each launch (tools)
 
@@ -128,12 +133,11 @@ def _upload(params, table, device, js, B, H):
 def _launch(params, table, ws, info, stream, phases):
     dev_tbl = 0  # NULL: by-value tables (the library uploads one itself if it needs it)
     saved = params.phases
-    steps = ((("score", N.PHASE_SCORE), ("select", N.PHASE_SELECT), ("gather", N.PHASE_GATHER))
-             if _timer is not None and _timer.split else (("all", phases),))
+    steps = _timer.steps if _timer is not None and _timer.split else (("all", phases),)
     for name, bits in steps:
         if not phases & bits:
             continue
-        params.phases = bits
+        params.phases = bits & phases
         if _timer is not None:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(stream)

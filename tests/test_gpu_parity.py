@@ -26,11 +26,13 @@ def _run_case(case, values):
     return tin, out
 
 
-@pytest.fixture(params=["fused", "kernels"])
+@pytest.fixture(params=["kernels", "separate", "fused"])
 def launch_path(request, monkeypatch):
-    """Both launch paths of kvc_launch: the fused persistent kernel (default for 128/256-byte
-    rows) and the three-kernel SCORE/SELECT/GATHER path (KVC_FUSED=0)."""
+    """Every launch path of kvc_launch: the default SCORE + SELECT_GATHER kernels ("kernels"),
+    SCORE / SELECT / GATHER as three kernels (KVC_SEL_GATHER=0, "separate"), and the opt-in
+    fused persistent kernel (KVC_FUSED=1, 128/256-byte rows)."""
     monkeypatch.setenv("KVC_FUSED", "1" if request.param == "fused" else "0")
+    monkeypatch.setenv("KVC_SEL_GATHER", "0" if request.param == "separate" else "1")
     return request.param
 
 
