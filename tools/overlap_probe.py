@@ -1,6 +1,7 @@
-"""Does SELECT overlap with SCORE when they run on two streams?  (GPU box, tuning aid.)
-Half the headline layers are scored on one stream while the other half's rows are selected on
-a second (high-priority) stream; compares with the same two launches back to back."""
+"""Does SELECT (+GATHER) overlap with SCORE when they run on two streams?  (GPU box, tuning aid.)
+Half the headline layers are scored on one stream while the other half's rows are selected
+(and gathered: the select_gather kernel, unless OVERLAP_PHASES=select) on a second stream
+(high priority unless OVERLAP_PRIO=0); compares with the same two launches back to back."""
 import json
 import os
 import sys
@@ -47,8 +48,9 @@ def run(tab, phases, stream):
 
 
 os.environ["KVC_FUSED"] = "0"
+SEL = N.PHASE_SELECT if os.environ.get("OVERLAP_PHASES") == "select" else (N.PHASE_SELECT | N.PHASE_GATHER)
 s1 = torch.cuda.Stream(device=dev)
-s2 = torch.cuda.Stream(device=dev, priority=-1)  # high priority
+s2 = torch.cuda.Stream(device=dev, priority=-1 if os.environ.get("OVERLAP_PRIO", "1") == "1" else 0)
 main = torch.cuda.current_stream(dev)
 run(A, N.PHASE_SCORE, main)  # norms of A for its select
 torch.cuda.synchronize()
@@ -61,19 +63,19 @@ for mode in ("serial", "overlap", "serial", "overlap"):
         e0.record(main)
         if mode == "serial":
             run(B, N.PHASE_SCORE, main)
-            run(A, N.PHASE_SELECT, main)
+            run(A, SEL, main)
         else:
             s1.wait_stream(main)
             s2.wait_stream(main)
             run(B, N.PHASE_SCORE, s1)
-            run(A, N.PHASE_SELECT, s2)
+            run(A, SEL, s2)
             main.wait_stream(s1)
             main.wait_stream(s2)
         e1.record(main)
         torch.cuda.synchronize()
         times.append(e0.elapsed_time(e1))
     res.setdefault(mode, []).append(sorted(times)[2])
-for nm, ph, tab in (("score_B_alone", N.PHASE_SCORE, B), ("select_A_alone", N.PHASE_SELECT, A)):
+for nm, ph, tab in (("score_B_alone", N.PHASE_SCORE, B), ("select_A_alone", SEL, A)):
     ts = []
     for _ in range(5):
         torch.cuda.synchronize()
@@ -84,4 +86,6 @@ for nm, ph, tab in (("score_B_alone", N.PHASE_SCORE, B), ("select_A_alone", N.PH
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
     res[nm] = sorted(ts)[2]
+res["phases"] = int(SEL)
+res["prio"] = os.environ.get("OVERLAP_PRIO", "1")
 print(json.dumps(res))

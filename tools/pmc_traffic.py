@@ -17,6 +17,9 @@ ALGO = {  # bytes per 32-layer launch of the headline workload
     "score_kernel": {"algorithmic_read": L * H * S * D * 2, "algorithmic_write": L * H * S * 2},
     "gather_kernel": {"algorithmic_read": 2 * L * H * K * D * 2,
                       "algorithmic_write": 2 * L * H * K * D * 2},
+    # norms read + kept K,V rows read; K,V out written (the index list stays in LDS)
+    "select_gather_kernel": {"algorithmic_read": L * H * S * 2 + 2 * L * H * K * D * 2,
+                             "algorithmic_write": 2 * L * H * K * D * 2},
 }
 vals = defaultdict(lambda: defaultdict(list))
 for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
