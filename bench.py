@@ -120,6 +120,49 @@ def cpu_baseline(seq_len=S, head_dim=D, seconds=12.0):
                       f"{torch.backends.cpu.get_cpu_capability()}"}
 
 
+def ppl_delta(device, tokens=256, fix=64, keep_ratio=0.5):
+    """The metric's "PPL delta vs ref" half: teacher-forced evaluate_with_compression (one
+    compress call per token) of a random-init GPT-NeoX (pythia architecture, 4 layers, weights
+    unavailable offline) on `device`, once with the engine's fix_size_l2_compress and once with
+    the reference's CPU op sequence (oracle/torch_port.py, K/V copied to the host and back) as
+    compress_fn; same model, same synthetic token stream."""
+    from transformers import GPTNeoXConfig, GPTNeoXForCausalLM
+    from kvcompress.evaluate import evaluate_with_compression
+    from kvcompress.methods import fix_size_l2_compress
+    from oracle.torch_port import fix_size_l2_layer
+
+    class Tok:  # deterministic byte-level token stream
+        def encode(self, text, return_tensors="pt"):
+            return torch.tensor([[(b * 7 + i) % 512 for i, b in enumerate(text.encode())]])
+
+    def reference(kv, skip_layers=(), fix_kv_size=fix, keep_ratio=keep_ratio):
+        out = []
+        for i, (k, v) in enumerate(kv):  # fix_size_l2.py:69-74 skip tests, then :99-150
+            if k.size(2) <= fix_kv_size or i in skip_layers:
+                out.append((k, v))
+                continue
+            kk, vv = fix_size_l2_layer(k.cpu(), v.cpu(), fix_kv_size, keep_ratio)
+            out.append((kk.to(k.device), vv.to(v.device)))
+        return out
+
+    torch.manual_seed(0)
+    cfg = GPTNeoXConfig(vocab_size=512, hidden_size=256, num_hidden_layers=4,
+                        num_attention_heads=4, intermediate_size=1024, rotary_pct=0.25,
+                        max_position_embeddings=4096)
+    model = GPTNeoXForCausalLM(cfg).to(torch.bfloat16).to(device).eval()
+    text = "The quick brown fox jumps over the lazy dog. " * (tokens // 40 + 1)
+    kw = dict(fix_kv_size=fix, keep_ratio=keep_ratio)
+    r = [evaluate_with_compression(model, Tok(), text, compress_fn=fn, compress_kwargs=kw,
+                                   max_tokens=tokens, skip_layers=[0], show_progress=False)
+         for fn in (fix_size_l2_compress, reference)]
+    return {"value": r[0]["perplexity"] - r[1]["perplexity"], "ppl": r[0]["perplexity"],
+            "ppl_ref": r[1]["perplexity"], "accuracy_delta": r[0]["accuracy"] - r[1]["accuracy"],
+            "tokens": r[0]["num_tokens"], "final_cache_size": r[0]["final_cache_size"],
+            "sample": f"fix_size_l2(fix_kv_size={fix}, keep_ratio={keep_ratio}), skip_layers=[0], "
+                      "random-init 4-layer GPT-NeoX (pythia arch) bf16, synthetic tokens; "
+                      "engine vs the reference's CPU op sequence as compress_fn"}
+
+
 def timed_steps(step, steps, warmup, dist, sync, device, on_start=None):
     """W untimed warmup steps, then exactly K timed steps bracketed by barrier + sync on both
     sides; returns the MAX elapsed seconds over ranks (all ranks return the same value)."""
@@ -281,6 +324,7 @@ def main():
         res["tokens_evicted_per_sec"] = ev * world * args.steps / elapsed
         if not args.no_cpu_baseline and method == "fix_size_l2":
             res["cpu_baseline"] = cpu_baseline(seq_len, head_dim)
+            res["ppl_delta_vs_ref"] = ppl_delta(dev)
         print(json.dumps(res), flush=True)
     if dist:
         dist.barrier()
