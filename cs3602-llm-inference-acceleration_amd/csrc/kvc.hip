@@ -57,6 +57,11 @@ struct DTypeTraits<KVC_BF16> {
   typedef uint16_t key_t;
 };
 template <>
+struct DTypeTraits<KVC_F16> {
+  static constexpr int esz = 2;
+  typedef uint16_t key_t;
+};
+template <>
 struct DTypeTraits<KVC_F32> {
   static constexpr int esz = 4;
   typedef uint32_t key_t;
@@ -66,24 +71,59 @@ template <int DT>
 __device__ __forceinline__ float load_dt(const char* base, int i) {
   if constexpr (DT == KVC_BF16)
     return bf16_to_f32(reinterpret_cast<const uint16_t*>(base)[i]);
+  else if constexpr (DT == KVC_F16)
+    return f16_to_f32(reinterpret_cast<const uint16_t*>(base)[i]);
   else
     return reinterpret_cast<const float*>(base)[i];
+}
+
+// storage bits of an fp32 value rounded to a 16-bit dtype (c10 conversions)
+template <int DT>
+__device__ __forceinline__ uint32_t bits16_dt(float f) {
+  if constexpr (DT == KVC_BF16)
+    return f32_to_bf16_rne(f);
+  else
+    return f32_to_f16_rne(f);
 }
 
 template <int DT>
 __device__ __forceinline__ float round_dt(float f) {
   if constexpr (DT == KVC_BF16)
     return bf16_to_f32(f32_to_bf16_rne(f));
+  else if constexpr (DT == KVC_F16)
+    return f16_to_f32(f32_to_f16_rne(f));
   else
     return f;
 }
 
+// sort key of a 16-bit storage pattern
+template <int DT>
+__device__ __forceinline__ uint16_t key16_dt(uint32_t bits, bool desc) {
+  if constexpr (DT == KVC_BF16)
+    return key_bf16(bits, desc);
+  else
+    return key_f16(bits, desc);
+}
+
 template <int DT>
 __device__ __forceinline__ typename DTypeTraits<DT>::key_t key_of(float f, bool desc) {
-  if constexpr (DT == KVC_BF16)
-    return key_bf16(f32_to_bf16_rne(f), desc);
-  else
+  if constexpr (DT == KVC_F32)
     return key_f32(f32_to_bits(f), desc);
+  else
+    return key16_dt<DT>(bits16_dt<DT>(f), desc);
+}
+
+// torch.gather's NaN rewrite on two 16-bit elements (bf16: 0xFFFF; fp16: quiet bit); fp32 none
+template <int DT>
+__device__ __forceinline__ uint4 canon_nan_dt(uint4 a) {
+  if constexpr (DT == KVC_BF16)
+    return make_uint4(canon_nan_bf16x2(a.x), canon_nan_bf16x2(a.y), canon_nan_bf16x2(a.z),
+                      canon_nan_bf16x2(a.w));
+  else if constexpr (DT == KVC_F16)
+    return make_uint4(canon_nan_f16x2(a.x), canon_nan_f16x2(a.y), canon_nan_f16x2(a.z),
+                      canon_nan_f16x2(a.w));
+  else
+    return a;
 }
 
 // Diagnostic build only (-DKVC_STAMPS): thread 0 of every select workgroup records s_memtime at
@@ -119,7 +159,19 @@ __device__ __forceinline__ void wave_sync() {
 // ---------------------------------------------------------------------------------------------
 template <int DT, int NC>
 __device__ __forceinline__ void accum_chunk(float (&acc)[8], const uint4 x, int gchunk) {
-  if constexpr (DT == KVC_BF16) {
+  if constexpr (DT == KVC_F16) {
+    // NormTwoOps<Half, float> (binary_kernel_reduce): ONE accumulator in dim order; x*x is exact
+    // in fp32 for an fp16 x, so the fma equals torch's acc + x*x.  (acc[1..7] stay 0: the final
+    // lane sum adds +0 to a non-negative sum, which changes nothing.)
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float e0 = (float)__builtin_bit_cast(_Float16, (uint16_t)(w[q] & 0xFFFFu));
+      const float e1 = (float)__builtin_bit_cast(_Float16, (uint16_t)(w[q] >> 16));
+      acc[0] = __builtin_fmaf(e0, e0, acc[0]);
+      acc[0] = __builtin_fmaf(e1, e1, acc[0]);
+    }
+  } else if constexpr (DT == KVC_BF16) {
     // chunk c holds elements 8c..8c+7: element e feeds accumulator e
     const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
@@ -139,7 +191,7 @@ __device__ __forceinline__ void accum_chunk(float (&acc)[8], const uint4 x, int 
 }
 
 // One 64-token tile of one (layer, b, h) row: coalesced 16-B loads -> per-wave LDS slab ->
-// one lane per token, torch.norm's 8-accumulator FMA order.  `wl` is this wave's slab
+// one lane per token, torch.norm's 8-accumulator FMA order (fp16: its serial order).  `wl` is this wave's slab
 // (kTile * ROWB bytes).  sc1 = publish the norms write-through for an in-launch consumer.
 template <int DT, int NC, bool NTL = false>
 __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int tt, int H,
@@ -199,9 +251,9 @@ __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int t
     for (int j = 1; j < 8; ++j) s = s + acc[j];
     const float r = __builtin_sqrtf(s);
     char* nrow = norms + (int64_t)(ly->row0 + row) * norm_stride * ESZ;
-    if constexpr (DT == KVC_BF16) {
+    if constexpr (DT != KVC_F32) {
       uint16_t* d = reinterpret_cast<uint16_t*>(nrow) + tok0 + lane;
-      const uint16_t val = (uint16_t)f32_to_bf16_rne(r);
+      const uint16_t val = (uint16_t)bits16_dt<DT>(r);
       if (sc1)
         __hip_atomic_store(d, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else
@@ -325,11 +377,12 @@ __device__ void snapkv_keys(const char* nrow, int n, int pool_k, bool desc, KeyT
     has_nan |= sc.fnan[w];
   }
   if (has_nan) mx = __builtin_nanf("");
-  const float m = round_dt<DT>(mx + 1e-6f);
+  // `max + 1e-6` (snapkv_lite.py:99): the python scalar takes the tensor's dtype first
+  const float m = round_dt<DT>(mx + round_dt<DT>(1e-6f));
   for (int i = tid; i < n; i += NT) {
     const float s = round_dt<DT>(m - load_dt<DT>(nrow, i));
-    if constexpr (DT == KVC_BF16)
-      reinterpret_cast<uint16_t*>(tmp)[i] = (uint16_t)f32_to_bf16_rne(s);
+    if constexpr (DT != KVC_F32)
+      reinterpret_cast<uint16_t*>(tmp)[i] = (uint16_t)bits16_dt<DT>(s);
     else
       reinterpret_cast<float*>(tmp)[i] = s;
   }
@@ -717,11 +770,11 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
       if (v < nvec) {
         const uint32_t w[4] = {buf[q].x, buf[q].y, buf[q].z, buf[q].w};
         uint32_t kw[4], iw[4];
-        if constexpr (DT == KVC_BF16) {
+        if constexpr (DT != KVC_F32) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            kw[e] = (uint32_t)key_bf16(w[e] & 0xFFFFu, desc) |
-                    ((uint32_t)key_bf16(w[e] >> 16, desc) << 16);
+            kw[e] = (uint32_t)key16_dt<DT>(w[e] & 0xFFFFu, desc) |
+                    ((uint32_t)key16_dt<DT>(w[e] >> 16, desc) << 16);
             iw[e] = (uint32_t)(v * 8 + 2 * e) | ((uint32_t)(v * 8 + 2 * e + 1) << 16);
           }
           *reinterpret_cast<uint4*>(key + v * 8) = make_uint4(kw[0], kw[1], kw[2], kw[3]);
@@ -916,13 +969,9 @@ __global__ void __launch_bounds__(kGatherThreads)
     const int u = threadIdx.x + i * kGatherThreads;
     if (u < nu) {
       uint4 a = xk[i], bq = xv[i];
-      if constexpr (DT == KVC_BF16) {
-        if (gat[i]) {  // torch.gather's bf16 NaN rewrite (gathered segment only)
-          a.x = canon_nan_bf16x2(a.x); a.y = canon_nan_bf16x2(a.y);
-          a.z = canon_nan_bf16x2(a.z); a.w = canon_nan_bf16x2(a.w);
-          bq.x = canon_nan_bf16x2(bq.x); bq.y = canon_nan_bf16x2(bq.y);
-          bq.z = canon_nan_bf16x2(bq.z); bq.w = canon_nan_bf16x2(bq.w);
-        }
+      if (gat[i]) {  // torch.gather's NaN rewrite (gathered segment only)
+        a = canon_nan_dt<DT>(a);
+        bq = canon_nan_dt<DT>(bq);
       }
       if constexpr (NTS) {
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -1030,13 +1079,9 @@ __device__ __forceinline__ void gather_row(const kvc_layer_t* __restrict__ ly, i
       const int u = u0 + tid0 + i * NT;
       if (u < nu) {
         uint4 a = xk[i], q = xv[i];
-        if constexpr (DT == KVC_BF16) {
-          if (gat[i]) {
-            a.x = canon_nan_bf16x2(a.x); a.y = canon_nan_bf16x2(a.y);
-            a.z = canon_nan_bf16x2(a.z); a.w = canon_nan_bf16x2(a.w);
-            q.x = canon_nan_bf16x2(q.x); q.y = canon_nan_bf16x2(q.y);
-            q.z = canon_nan_bf16x2(q.z); q.w = canon_nan_bf16x2(q.w);
-          }
+        if (gat[i]) {
+          a = canon_nan_dt<DT>(a);
+          q = canon_nan_dt<DT>(q);
         }
         if constexpr (NTS) {  // written once: non-temporal
           typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -1201,18 +1246,28 @@ __global__ void __launch_bounds__(NT, 8)
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
-static inline int esize(int dtype) { return dtype == KVC_BF16 ? 2 : 4; }
+static inline int esize(int dtype) { return dtype == KVC_F32 ? 4 : 2; }
+// Calls f(std::integral_constant<int, DT>) for the call's storage dtype (validated by plan_impl).
+template <typename F>
+static void with_dtype(int dtype, F&& f) {
+  if (dtype == KVC_BF16)
+    f(std::integral_constant<int, KVC_BF16>());
+  else if (dtype == KVC_F16)
+    f(std::integral_constant<int, KVC_F16>());
+  else
+    f(std::integral_constant<int, KVC_F32>());
+}
 static inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 // one row of the global selection scratch (SelArrays for n_cap positions), 256-B aligned rows
 static inline size_t sel_scratch_row_bytes(int n_cap, int dtype) {
-  return round_up(sel_bytes(n_cap, dtype == KVC_BF16 ? 2 : 4, n_cap / 2 + 1), 256);
+  return round_up(sel_bytes(n_cap, esize(dtype), n_cap / 2 + 1), 256);
 }
 
 static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_plan_info_t* info,
                      bool fill) {
   if (!p || nl < 0 || (nl > 0 && !layers)) return KVC_E_ARG;
-  if (p->dtype != KVC_BF16 && p->dtype != KVC_F32) return KVC_E_DTYPE;
+  if (p->dtype != KVC_BF16 && p->dtype != KVC_F16 && p->dtype != KVC_F32) return KVC_E_DTYPE;
   if (p->batch < 1 || p->heads < 1 || p->head_dim < 1) return KVC_E_ARG;
   if (p->order != KVC_ASC && p->order != KVC_DESC) return KVC_E_ARG;
   if (p->algo != KVC_ALGO_SORT && p->algo != KVC_ALGO_TOPK) return KVC_E_ARG;
@@ -1373,7 +1428,7 @@ const char* kvc_status_string(int s) {
   switch (s) {
     case KVC_OK: return "ok";
     case KVC_E_ARG: return "invalid argument";
-    case KVC_E_DTYPE: return "unsupported dtype (bf16/fp32 only)";
+    case KVC_E_DTYPE: return "unsupported dtype (bf16/fp16/fp32 only)";
     case KVC_E_HEADDIM: return "unsupported head_dim";
     case KVC_E_ALIGN: return "pointer or stride not 16-byte aligned";
     case KVC_E_TOO_LONG: return "scored zone longer than kvc_max_zone_len()";
@@ -1457,11 +1512,10 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
   hipLaunchKernelGGL((fused_kernel<DT_, NC_>), grid, block, 0, s, layers_dev, nl, H, BH,       \
                      p->order, p->algo, norms, info.norm_row_stride, ctl, wave_seg,             \
                      (int)info.score_tiles, (int)info.rows, n_score_first, diag, tl)
-    if (p->dtype == KVC_BF16) {
-      if (nc == 8) { KVC_FUSED_LAUNCH(KVC_BF16, 8); } else { KVC_FUSED_LAUNCH(KVC_BF16, 16); }
-    } else {
-      if (nc == 8) { KVC_FUSED_LAUNCH(KVC_F32, 8); } else { KVC_FUSED_LAUNCH(KVC_F32, 16); }
-    }
+    with_dtype(p->dtype, [&](auto dt) {
+      constexpr int DT = decltype(dt)::value;
+      if (nc == 8) { KVC_FUSED_LAUNCH(DT, 8); } else { KVC_FUSED_LAUNCH(DT, 16); }
+    });
 #undef KVC_FUSED_LAUNCH
     return hipGetLastError() == hipSuccess ? KVC_OK : KVC_E_HIP;
   }
@@ -1481,12 +1535,11 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
       max_out = layers[l].n_out > max_out ? layers[l].n_out : max_out;
     }
     if ((p->phases & KVC_PHASE_SCORE) && tile_end > tile_base && !p->external_index) {
-      if (p->dtype == KVC_BF16)
-        dispatch_nc<KVC_BF16>(nc, true, T, cn, H, BH, tile_base, tile_end - tile_base, norms,
-                              info.norm_row_stride, idx, info.index_row_stride, s);
-      else
-        dispatch_nc<KVC_F32>(nc, true, T, cn, H, BH, tile_base, tile_end - tile_base, norms,
-                             info.norm_row_stride, idx, info.index_row_stride, s);
+      with_dtype(p->dtype, [&](auto dt) {
+        dispatch_nc<decltype(dt)::value>(nc, true, T, cn, H, BH, tile_base, tile_end - tile_base,
+                                         norms, info.norm_row_stride, idx, info.index_row_stride,
+                                         s);
+      });
     }
     if ((p->phases & KVC_PHASE_SELECT) && sel && !p->external_index && long_zone) {
       const dim3 grid((unsigned)(cn * BH)), block(kSelThreads);
@@ -1494,18 +1547,15 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
       char* scratch = w + round_up(info.index_offset +
                                    (size_t)info.rows * info.index_row_stride * 4, 256);
       const int64_t rb = (int64_t)sel_scratch_row_bytes(n_cap, p->dtype);
-      if (p->dtype == KVC_BF16)
-        hipLaunchKernelGGL(select_global_kernel<KVC_BF16>, grid, block, 0, s, T, BH, p->order,
-                           p->algo, norms, info.norm_row_stride, idx, info.index_row_stride,
-                           wave_seg, scratch, rb, n_cap);
-      else
-        hipLaunchKernelGGL(select_global_kernel<KVC_F32>, grid, block, 0, s, T, BH, p->order,
-                           p->algo, norms, info.norm_row_stride, idx, info.index_row_stride,
-                           wave_seg, scratch, rb, n_cap);
+      with_dtype(p->dtype, [&](auto dt) {
+        hipLaunchKernelGGL(select_global_kernel<decltype(dt)::value>, grid, block, 0, s, T, BH,
+                           p->order, p->algo, norms, info.norm_row_stride, idx,
+                           info.index_row_stride, wave_seg, scratch, rb, n_cap);
+      });
     } else if ((p->phases & KVC_PHASE_SELECT) && sel && !p->external_index) {
       uint64_t* st = stamps ? stamps + (size_t)layers[c0].row0 * 32 : nullptr;
       const int n_cap = (int)info.norm_row_stride;  // longest zone of the call, rounded to 64
-      const int ks = p->dtype == KVC_BF16 ? 2 : 4;
+      const int ks = esize(p->dtype);
       const char* ent = getenv("KVC_SEL_NT");  // tuning only: 1024 = no small variant
       const bool small = n_cap <= kSmallZone && !(ent && atoi(ent) == 1024);
       const int cap = small ? sel_cap(n_cap, ks) : 0;
@@ -1518,11 +1568,10 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
 #define KVC_SG(DT_, NT_)                                                                      \
   launch_select_gather<DT_, NT_>(nc, T, cn, H, BH, p->order, p->algo, norms,                   \
                                  info.norm_row_stride, wave_seg, n_cap, cap, lds, s)
-        if (p->dtype == KVC_BF16) {
-          if (small) KVC_SG(KVC_BF16, kSelThreadsSmall); else KVC_SG(KVC_BF16, kSelThreads);
-        } else {
-          if (small) KVC_SG(KVC_F32, kSelThreadsSmall); else KVC_SG(KVC_F32, kSelThreads);
-        }
+        with_dtype(p->dtype, [&](auto dt) {
+          constexpr int DT = decltype(dt)::value;
+          if (small) KVC_SG(DT, kSelThreadsSmall); else KVC_SG(DT, kSelThreads);
+        });
 #undef KVC_SG
         continue;  // this chunk's gather is done
       }
@@ -1531,22 +1580,18 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
   hipLaunchKernelGGL((select_kernel<DT_, NT_>), grid, dim3(NT_), lds, s, T, BH, p->order,    \
                      p->algo, norms, info.norm_row_stride, idx, info.index_row_stride,       \
                      wave_seg, n_cap, cap, st)
-      if (p->dtype == KVC_BF16) {
-        if (small) KVC_SEL_LAUNCH(KVC_BF16, kSelThreadsSmall);
-        else KVC_SEL_LAUNCH(KVC_BF16, kSelThreads);
-      } else {
-        if (small) KVC_SEL_LAUNCH(KVC_F32, kSelThreadsSmall);
-        else KVC_SEL_LAUNCH(KVC_F32, kSelThreads);
-      }
+      with_dtype(p->dtype, [&](auto dt) {
+        constexpr int DT = decltype(dt)::value;
+        if (small) KVC_SEL_LAUNCH(DT, kSelThreadsSmall);
+        else KVC_SEL_LAUNCH(DT, kSelThreads);
+      });
 #undef KVC_SEL_LAUNCH
     }
     if ((p->phases & KVC_PHASE_GATHER) && max_out > 0) {
-      if (p->dtype == KVC_BF16)
-        dispatch_nc<KVC_BF16>(nc, false, T, cn, H, BH, 0, max_out, norms, info.norm_row_stride,
-                              idx, info.index_row_stride, s);
-      else
-        dispatch_nc<KVC_F32>(nc, false, T, cn, H, BH, 0, max_out, norms, info.norm_row_stride,
-                             idx, info.index_row_stride, s);
+      with_dtype(p->dtype, [&](auto dt) {
+        dispatch_nc<decltype(dt)::value>(nc, false, T, cn, H, BH, 0, max_out, norms,
+                                         info.norm_row_stride, idx, info.index_row_stride, s);
+      });
     }
   }
   return hipGetLastError() == hipSuccess ? KVC_OK : KVC_E_HIP;

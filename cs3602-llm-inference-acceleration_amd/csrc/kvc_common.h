@@ -2,6 +2,7 @@
 //
 // Everything here reproduces a PyTorch CPU behaviour the reference relies on:
 //   * c10::BFloat16 round-to-nearest-even with NaN -> 0x7FC0 (c10/util/BFloat16.h)
+//   * c10::Half conversions (IEEE binary16, round-to-nearest-even, NaN -> 0x7E00 | sign)
 //   * the total order PyTorch's sort/topk comparators induce on float keys
 //     (aten SortingUtils.h KeyValueCompAsc / KeyValueCompDesc, TopKImpl.h), mapped to unsigned
 //     integers so the selection kernels compare keys with a single integer '<'.
@@ -34,16 +35,50 @@ KVC_HD uint32_t f32_to_bf16_rne(float f) {
   return u >> 16;
 }
 
+// IEEE binary16 -> fp32, exact (subnormals: man * 2^-24 is exact and normal in fp32)
+KVC_HD float f16_to_f32(uint32_t h) {
+  const uint32_t sign = (h & 0x8000u) << 16;
+  const uint32_t e = (h >> 10) & 0x1Fu, man = h & 0x3FFu;
+  if (e == 0x1Fu) return bits_to_f32(sign | 0x7F800000u | (man << 13));
+  if (e == 0) {
+    const float f = (float)man * 5.9604644775390625e-8f;  // 2^-24
+    return sign ? -f : f;
+  }
+  return bits_to_f32(sign | ((e + 112u) << 23) | (man << 13));
+}
+
+// c10::Half(float) (fp16_ieee_from_fp32_value): round to nearest even, NaN -> 0x7E00 | sign;
+// integer arithmetic only, so it does not depend on the FP mode or denormal flushing.
+KVC_HD uint32_t f32_to_f16_rne(float f) {
+  const uint32_t u = f32_to_bits(f);
+  const uint32_t sign = (u >> 16) & 0x8000u;
+  const uint32_t a = u & 0x7FFFFFFFu;
+  if (a > 0x7F800000u) return sign | 0x7E00u;
+  if (a >= 0x477FF000u) return sign | 0x7C00u;  // >= 65520 rounds to inf
+  if (a >= 0x38800000u)                         // normal binary16
+    return sign | (((a + 0xFFFu + ((a >> 13) & 1u)) >> 13) - (112u << 10));
+  // subnormal binary16: units of 2^-24, RNE on the shifted-out bits
+  const uint32_t e = a >> 23;
+  if (e < 102u) return sign;  // below 2^-25: rounds to zero (2^-25 itself ties to even 0)
+  const uint32_t m = (a & 0x7FFFFFu) | 0x800000u;
+  const uint32_t sh = 126u - e;  // 14..24
+  uint32_t r = m >> sh;
+  const uint32_t rem = m & ((1u << sh) - 1u), half = 1u << (sh - 1u);
+  r += (rem > half || (rem == half && (r & 1u))) ? 1u : 0u;
+  return sign | r;
+}
+
 // Sort keys.  Ascending base order is PyTorch's asc comparator
 //   (!isnan(a) && isnan(b)) || a < b
 // i.e. numeric order with -0 == +0 and every NaN tied above +inf.  Descending order
 //   (isnan(a) && !isnan(b)) || a > b
 // is the exact reverse (NaN first), obtained by complementing the key.  Equal keys <=> the
 // comparator considers the two elements equivalent, so tie dynamics are preserved exactly.
-KVC_HD uint16_t key_bf16(uint32_t b, bool desc) {
+// 16-bit storage formats differ only in where NaN starts: bf16 above 0x7F80, fp16 above 0x7C00.
+KVC_HD uint16_t key_h16(uint32_t b, bool desc, uint32_t inf_bits) {
   b &= 0xFFFFu;
   uint32_t k;
-  if ((b & 0x7FFFu) > 0x7F80u) {
+  if ((b & 0x7FFFu) > inf_bits) {
     k = 0xFFFFu;
   } else {
     if (b == 0x8000u) b = 0;
@@ -51,6 +86,8 @@ KVC_HD uint16_t key_bf16(uint32_t b, bool desc) {
   }
   return (uint16_t)(desc ? (~k & 0xFFFFu) : k);
 }
+KVC_HD uint16_t key_bf16(uint32_t b, bool desc) { return key_h16(b, desc, 0x7F80u); }
+KVC_HD uint16_t key_f16(uint32_t b, bool desc) { return key_h16(b, desc, 0x7C00u); }
 
 KVC_HD uint32_t key_f32(uint32_t b, bool desc) {
   uint32_t k;
@@ -69,6 +106,15 @@ KVC_HD uint32_t canon_nan_bf16x2(uint32_t w) {
   uint32_t lo = w & 0xFFFFu, hi = w >> 16;
   if ((lo & 0x7FFFu) > 0x7F80u) lo = 0xFFFFu;
   if ((hi & 0x7FFFu) > 0x7F80u) hi = 0xFFFFu;
+  return lo | (hi << 16);
+}
+
+// torch.gather on CPU quiets every fp16 NaN (sets bit 9: 0x7C01 -> 0x7E01; measured over all
+// 65536 patterns); applied to the gathered segment of fp16 outputs only.
+KVC_HD uint32_t canon_nan_f16x2(uint32_t w) {
+  uint32_t lo = w & 0xFFFFu, hi = w >> 16;
+  if ((lo & 0x7FFFu) > 0x7C00u) lo |= 0x200u;
+  if ((hi & 0x7FFFu) > 0x7C00u) hi |= 0x200u;
   return lo | (hi << 16);
 }
 

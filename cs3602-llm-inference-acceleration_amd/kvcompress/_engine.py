@@ -38,7 +38,7 @@ class Segments:
     ext_index: Optional[torch.Tensor] = None  # [B, H, n_select] int64 zone-local, ascending
 
 
-_SUPPORTED = {torch.bfloat16: N.KVC_BF16, torch.float32: N.KVC_F32}
+_SUPPORTED = {torch.bfloat16: N.KVC_BF16, torch.float16: N.KVC_F16, torch.float32: N.KVC_F32}
 
 
 class PhaseTimer:
@@ -83,7 +83,7 @@ def _check_tensors(j: Segments):
             "(no CPU fallback).")
     if k.dtype not in _SUPPORTED or v.dtype != k.dtype:
         raise TypeError(
-            f"kvcompress (MI355X HIP engine) supports bfloat16/float32 K and V of one dtype; "
+            f"kvcompress (MI355X HIP engine) supports bfloat16/float16/float32 K and V of one dtype; "
             f"layer {j.layer_idx} has {k.dtype}/{v.dtype}")
     if k.dim() != 4 or v.shape != k.shape:
         raise ValueError(f"layer {j.layer_idx}: K/V must both be [B, H, S, D]; got "

@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_HERE, "_lib", "libkvc.so")
 # diagnostic builds (e.g. the s_memtime-stamped select kernel) may be swapped in by path
 LIB_PATH = os.environ.get("KVC_LIB", LIB_PATH)
 
-KVC_F32, KVC_BF16 = 0, 1
+KVC_F32, KVC_BF16, KVC_F16 = 0, 1, 2
 KVC_ASC, KVC_DESC = 0, 1
 KVC_ALGO_SORT, KVC_ALGO_TOPK = 0, 1
 KVC_SCORE_NORM, KVC_SCORE_SNAPKV = 0, 1

@@ -46,7 +46,10 @@ extern "C" {
 
 typedef struct ihipStream_t* kvc_stream_t; /* a hipStream_t; NULL = legacy default stream */
 
-enum kvc_dtype { KVC_F32 = 0, KVC_BF16 = 1 };
+/* KVC_F16: IEEE half (what transformers >= 5 loads pythia checkpoints as: dtype="auto").  Its
+ * norm follows torch's non-vectorised CPU reduction (one fp32 accumulator in dim order), not the
+ * 8-lane order of bf16/fp32 -- see DESIGN.md. */
+enum kvc_dtype { KVC_F32 = 0, KVC_BF16 = 1, KVC_F16 = 2 };
 /* KVC_ASC keeps the smallest keys (argsort ascending, "keep_low");
  * KVC_DESC keeps the largest (argsort descending / topk largest, "keep_high", snapkv). */
 enum kvc_order { KVC_ASC = 0, KVC_DESC = 1 };
@@ -64,7 +67,7 @@ enum kvc_phase {
 enum kvc_status {
   KVC_OK = 0,
   KVC_E_ARG = -1,       /* malformed layer table / params                             */
-  KVC_E_DTYPE = -2,     /* dtype is not bf16 / fp32                                   */
+  KVC_E_DTYPE = -2,     /* dtype is not bf16 / fp16 / fp32                            */
   KVC_E_HEADDIM = -3,   /* head_dim*elem_size not in {128,160,256,320,512} bytes      */
   KVC_E_ALIGN = -4,     /* a base pointer or stride is not 16-byte aligned            */
   KVC_E_TOO_LONG = -5,  /* a scored zone is longer than kvc_max_zone_len() (65536)    */

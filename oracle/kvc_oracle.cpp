@@ -8,10 +8,14 @@
 // tests/test_oracle_golden.py checks this restatement against every one of them.
 //
 // What is restated (reference call sites in brackets):
-//   * torch.norm(x, p=2, dim=-1) for fp32/bf16 rows          [methods/fix_size_l2.py:106,
+//   * torch.norm(x, p=2, dim=-1)                               [methods/fix_size_l2.py:106,
 //     l2_compress.py:228, h2o_l2.py:296, snapkv_lite.py:96, pyramid_kv.py:313, adaptive_l2.py:473,527]
+//     fp32/bf16 rows (aten's vectorised reduce-lastdim norm_two_reduce_step)
 //     = 8 fp32 lane accumulators, lane j: acc_j = fma(x[d], x[d], acc_j) for d = j, j+8, ...;
 //       serial lane sum ((a0+a1)+a2)+...+a7; correctly rounded fp32 sqrt; RNE to the storage dtype.
+//     fp16 rows (not on that fast path: binary_kernel_reduce with NormTwoOps<Half, float>)
+//     = one fp32 accumulator over d = 0..D-1 (x*x is exact in fp32 for fp16 x, so fused or not
+//       is the same); correctly rounded fp32 sqrt; RNE to fp16.  0 mismatches / 14 M rows here.
 //   * Tensor.argsort(dim=-1[, descending]) (stable=False)     [fix_size_l2.py:107,113 ...]
 //     = libstdc++ std::sort on (key, index) pairs with PyTorch's key-only comparators
 //       asc: (!isnan(a) && isnan(b)) || a < b        desc: (isnan(a) && !isnan(b)) || a > b
@@ -20,6 +24,8 @@
 //       NaN-first '>' comparator (aten TopKImpl.h).
 //   * snapkv scoring: max(dim)+1e-6, subtraction, avg_pool1d(k, stride 1, pad k//2,
 //     count_include_pad)                                       [snapkv_lite.py:99-121]
+//     The python scalar 1e-6 is cast to the tensor's dtype before the fp32 add (type promotion
+//     of a wrapped number): bf16(1e-6) / fp16(1e-6), visible at the bottom of the range.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -29,7 +35,7 @@
 
 namespace {
 
-enum { DT_F32 = 0, DT_BF16 = 1 };
+enum { DT_F32 = 0, DT_BF16 = 1, DT_F16 = 2 };
 
 inline float bf16_to_f32(uint16_t b) {
   uint32_t u = static_cast<uint32_t>(b) << 16;
@@ -47,19 +53,61 @@ inline uint16_t f32_to_bf16(float f) {
   return static_cast<uint16_t>(u >> 16);
 }
 
-inline float load_val(int dtype, const void* p, int64_t i) {
-  return dtype == DT_BF16 ? bf16_to_f32(static_cast<const uint16_t*>(p)[i])
-                          : static_cast<const float*>(p)[i];
+// IEEE binary16 -> fp32 (exact, subnormals included)
+inline float f16_to_f32(uint16_t h) {
+  const uint32_t sign = static_cast<uint32_t>(h & 0x8000u) << 16;
+  const int exp = (h >> 10) & 0x1F;
+  const uint32_t man = h & 0x3FFu;
+  float f;
+  if (exp == 0x1F) {
+    const uint32_t u = sign | 0x7F800000u | (man << 13);
+    std::memcpy(&f, &u, 4);
+  } else if (exp == 0) {
+    f = std::ldexp(static_cast<float>(man), -24);
+    if (sign) f = -f;
+  } else {
+    const uint32_t u = sign | (static_cast<uint32_t>(exp + 112) << 23) | (man << 13);
+    std::memcpy(&f, &u, 4);
+  }
+  return f;
 }
 
-// Round an fp32 result to the storage dtype and back (what a bf16 tensor op does).
+// c10::Half(float): IEEE round to nearest even (fp16_ieee_from_fp32_value); NaN -> 0x7E00|sign
+inline uint16_t f32_to_f16(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  const uint16_t sign = static_cast<uint16_t>((u >> 16) & 0x8000u);
+  const uint32_t a = u & 0x7FFFFFFFu;
+  if (a > 0x7F800000u) return sign | 0x7E00u;
+  if (a >= 0x477FF000u) return sign | 0x7C00u;  // rounds to >= 65520: inf
+  if (a < 0x38800000u) {                         // below 2^-14: subnormal (or zero)
+    // value / 2^-24 rounded to nearest even integer
+    const float q = std::fabs(f) * 16777216.0f;  // exact: scaling by a power of two
+    const float r = std::nearbyint(q);           // default rounding mode: ties to even
+    return sign | static_cast<uint16_t>(r);
+  }
+  const uint32_t m = a + 0xFFFu + ((a >> 13) & 1u);  // RNE on the 13 dropped bits
+  return sign | static_cast<uint16_t>((m >> 13) - (112u << 10));
+}
+
+inline float load_val(int dtype, const void* p, int64_t i) {
+  if (dtype == DT_BF16) return bf16_to_f32(static_cast<const uint16_t*>(p)[i]);
+  if (dtype == DT_F16) return f16_to_f32(static_cast<const uint16_t*>(p)[i]);
+  return static_cast<const float*>(p)[i];
+}
+
+// Round an fp32 result to the storage dtype and back (what a bf16 / fp16 tensor op does).
 inline float round_dtype(int dtype, float f) {
-  return dtype == DT_BF16 ? bf16_to_f32(f32_to_bf16(f)) : f;
+  if (dtype == DT_BF16) return bf16_to_f32(f32_to_bf16(f));
+  if (dtype == DT_F16) return f16_to_f32(f32_to_f16(f));
+  return f;
 }
 
 inline void store_val(int dtype, void* p, int64_t i, float f) {
   if (dtype == DT_BF16)
     static_cast<uint16_t*>(p)[i] = f32_to_bf16(f);
+  else if (dtype == DT_F16)
+    static_cast<uint16_t*>(p)[i] = f32_to_f16(f);
   else
     static_cast<float*>(p)[i] = f;
 }
@@ -83,9 +131,27 @@ extern "C" {
 
 int orc_version(void) { return 1; }
 
+// Storage rounding of fp32 values (bit patterns out), for the conversion tests.
+int orc_to_dtype_bits(int dtype, const float* in, int64_t n, uint32_t* out) {
+  for (int64_t i = 0; i < n; ++i)
+    out[i] = dtype == DT_BF16 ? f32_to_bf16(in[i]) : dtype == DT_F16 ? f32_to_f16(in[i]) : 0u;
+  return 0;
+}
+
 // torch.norm(x, p=2, dim=-1) on rows of length D (row_stride in elements).
 int orc_row_norms(int dtype, const void* x, int64_t rows, int64_t D, int64_t row_stride,
                   void* out) {
+  if (dtype == DT_F16) {  // NormTwoOps<Half, float>: acc + x*x in dim order
+    for (int64_t r = 0; r < rows; ++r) {
+      float acc = 0.0f;
+      for (int64_t d = 0; d < D; ++d) {
+        const float v = load_val(dtype, x, r * row_stride + d);
+        acc = acc + v * v;
+      }
+      store_val(dtype, out, r, std::sqrt(acc));
+    }
+    return 0;
+  }
   if (D % 8 != 0) return -1;
   for (int64_t r = 0; r < rows; ++r) {
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -155,7 +221,9 @@ int orc_snapkv_scores(int dtype, const void* norms, int64_t n, int64_t pool_k, v
     if (v > mx) mx = v;
   }
   if (has_nan) mx = NAN;
-  const float m = round_dtype(dtype, mx + static_cast<float>(1e-6));
+  // `max + 1e-6`: the wrapped python scalar takes the tensor's dtype first
+  const float eps = round_dtype(dtype, static_cast<float>(1e-6));
+  const float m = round_dtype(dtype, mx + eps);
   std::vector<float> s(n);
   for (int64_t i = 0; i < n; ++i) s[i] = round_dtype(dtype, m - load_val(dtype, norms, i));
   if (pool_k > 1 && n >= pool_k) {

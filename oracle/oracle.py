@@ -9,7 +9,7 @@ Pinning: tests/test_oracle_golden.py checks every function below against the gol
 tests/golden/, which tests/golden/gen_goldens.py produced by running the unmodified reference.
 
 Representation: a layer is a pair (K, V) of numpy arrays [B, H, S, D]; bf16 tensors are uint16
-bit patterns, fp32 tensors are float32.  Every function mirrors its reference's control flow
+bit patterns, fp16 tensors are float16, fp32 tensors are float32.  Every function mirrors its reference's control flow
 line by line (file:line citations are to /root/reference/kvcompress/methods/).
 Each returned layer is tagged with how the reference produced it:
   "same" - the input tensor objects themselves (layer untouched),
@@ -25,7 +25,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
 
-DT_F32, DT_BF16 = 0, 1
+DT_F32, DT_BF16, DT_F16 = 0, 1, 2
 
 
 def lib():
@@ -42,6 +42,7 @@ def lib():
         _LIB.orc_topk.argtypes = [ctypes.c_int, vp, i64, i64, ctypes.c_int, vp]
         _LIB.orc_snapkv_scores.argtypes = [ctypes.c_int, vp, i64, i64, vp]
         _LIB.orc_antiqsort.argtypes = [i64, ctypes.c_int, i64, vp]
+        _LIB.orc_to_dtype_bits.argtypes = [ctypes.c_int, vp, i64, vp]
     return _LIB
 
 
@@ -50,7 +51,9 @@ def _dt(arr):
         return DT_BF16
     if arr.dtype == np.float32:
         return DT_F32
-    raise TypeError(f"oracle supports bf16 (uint16 bits) and float32, got {arr.dtype}")
+    if arr.dtype == np.float16:
+        return DT_F16
+    raise TypeError(f"oracle supports bf16 (uint16 bits), float16 and float32, got {arr.dtype}")
 
 
 def _ptr(a):
@@ -116,14 +119,18 @@ def snapkv_scores(prefix_norms, pool_k):
 def gather(X, idx):
     """torch.gather(X, 2, idx[..., None].expand(..., D)).
 
-    torch's CPU gather rewrites every bf16 NaN bit pattern to 0xFFFF (measured over all 65536
-    patterns; fp32 payloads and torch.cat copies are untouched), so the gathered segment of a
-    bf16 output carries 0xFFFF wherever the source held a NaN.
+    torch's CPU gather rewrites every bf16 NaN bit pattern to 0xFFFF and quiets every fp16 NaN
+    (sets bit 9: 0x7C01 -> 0x7E01), measured over all 65536 patterns of each; fp32 payloads and
+    torch.cat copies are untouched.  The gathered segment of an output carries the rewritten
+    patterns wherever the source held a NaN.
     """
     B, H = idx.shape[:2]
     out = X[np.arange(B)[:, None, None], np.arange(H)[None, :, None], idx, :]
     if out.dtype == np.uint16:
         out = np.where((out & 0x7FFF) > 0x7F80, np.uint16(0xFFFF), out).astype(np.uint16)
+    elif out.dtype == np.float16:
+        b = out.view(np.uint16)
+        out = np.where((b & 0x7FFF) > 0x7C00, b | np.uint16(0x200), b).astype(np.uint16).view(np.float16)
     return out
 
 

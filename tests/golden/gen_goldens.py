@@ -1,7 +1,7 @@
 """Generate golden fixtures by running the UNMODIFIED reference kvcompress (build container only).
 
     cd /root/repo && PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 \
-        python tests/golden/gen_goldens.py
+        python tests/golden/gen_goldens.py [--prims-only]
 
 The reference is imported from /root/reference (read-only); nothing of it is copied.  Outputs
 (data only) go to tests/golden/:
@@ -9,7 +9,8 @@ The reference is imported from /root/reference (read-only); nothing of it is cop
                    layer the output kind (same/view/new), shapes and SHA-256 of K_out/V_out bytes
   positions.npz  - per case/layer: source sequence position of every output row [B,H,n_out],
                    recovered by re-running the reference with position-encoding values
-  prims.json / prims.npz - torch.norm / argsort / topk outputs on tie-heavy rows
+  prims.json / prims.npz - torch.norm / argsort / topk outputs on tie-heavy rows, and the
+                   snapkv_lite scoring tensors (max + 1e-6, scores, pooled) per dtype
 Inputs are regenerated from tests/golden/prng.py recipes (hashes stored to detect drift).
 """
 import hashlib
@@ -39,7 +40,7 @@ def sha(a):
 
 def to_torch(a, dtype):
     t = torch.from_numpy(np.ascontiguousarray(a))
-    return t.view(torch.bfloat16) if dtype == "bf16" else t
+    return t.view(torch.bfloat16) if dtype == "bf16" else t  # fp16: numpy float16 -> torch.half
 
 
 def to_np(t, dtype):
@@ -177,6 +178,49 @@ def build_cases():
     add("recent_only", {"window_size": 512}, "bf16",
         [L((1, 2, 1024, 64), s + 120), L((1, 2, 1024, 64), s + 121),
          L((1, 2, 1024, 64), s + 122), L((1, 2, 300, 64), s + 123)], "default")
+    # ---- fp16 K/V (what transformers 5 loads pythia checkpoints as: dtype="auto" -> float16)
+    # and the snapkv epsilon at the bottom of each dtype's range (appended: earlier ids stay) ----
+    f = "fp16"
+    add("fix_size_l2", {"fix_kv_size": 512, "keep_ratio": 0.0, "strategy": "keep_low",
+                        "skip_layers": []}, f, [L((1, 32, 4096, 128), s + 130)], "cfg2")
+    for D in (64, 80, 128):
+        for var in ("normal", "scaled", "few", "special"):
+            add("fix_size_l2", {"fix_kv_size": 256, "keep_ratio": 0.5, "strategy": "keep_low"},
+                f, [L((1, 4, 700, D), s + 131 + D), L((2, 3, 1500, D), s + 132 + D, var)],
+                f"D{D}_{var}")
+    add("fix_size_l2", {"fix_kv_size": 300, "keep_ratio": 0.0, "strategy": "keep_high",
+                        "skip_layers": [1]}, f,
+        [L((1, 4, 1000, 128), s + 133), L((1, 4, 1000, 128), s + 134),
+         L((1, 4, 2000, 128), s + 135, "few")], "keep_high")
+    add("fix_size_l2", {"fix_kv_size": 64, "keep_ratio": 0.3, "strategy": "keep_low",
+                        "skip_layers": []}, f,
+        [L((1, 2, 5000, 64), s + 136, "equal"), L((1, 2, 65, 64), s + 137)], "equal_edge")
+    add("l2_compress", {"keep_ratio": 0.8, "prune_after": 100}, f,
+        [L((1, 4, 1000, 128), s + 140), L((1, 4, 1000, 128), s + 141),
+         L((1, 4, 1000, 128), s + 142, "special"), L((1, 4, 90, 128), s + 143)], "cfg1")
+    add("streaming_llm", {"start_size": 4, "recent_size": 1020}, f,
+        [L((1, 4, 2048, 128), s + 144), L((1, 4, 1000, 128), s + 145, "special")], "cfg3")
+    for D in (64, 80, 128):
+        add("h2o_l2", {"start_size": 4, "heavy_hitter_size": 64, "recent_size": 444}, f,
+            [L((1, 4, 2048, D), s + 150 + D), L((1, 4, 600, D), s + 151 + D, "few"),
+             L((1, 4, 513, D), s + 152 + D, "special")], f"cfg4_D{D}")
+    for var in ("normal", "few", "tiny", "micro", "zero", "special"):
+        add("snapkv_lite", {"observation_window": 32, "keep_size": 512, "pooling_kernel": 5},
+            f, [L((1, 4, 2048, 128), s + 160), L((1, 4, 1500, 80), s + 161, var)],
+            f"cfg5_{var}")
+    add("snapkv_lite", {"observation_window": 8, "keep_size": 40, "pooling_kernel": 4}, f,
+        [L((1, 4, 4096, 64), s + 162), L((1, 2, 2048, 64), s + 163, "few")], "partialsort_even")
+    for dt in ("bf16", "fp32"):
+        add("snapkv_lite", {"observation_window": 32, "keep_size": 512, "pooling_kernel": 5},
+            dt, [L((1, 4, 1500, 80), s + 164, "micro"), L((1, 4, 700, 128), s + 165, "micro")],
+            "cfg5_micro")
+    add("pyramid_kv", {"base_size": 512, "layer_decay": 0.9}, f,
+        [L((1, 4, 1024, 128), s + 170 + j) for j in range(6)], "cfg5")
+    add("adaptive_l2", {"target_size": 512}, f,
+        [L((1, 4, 2048, 128), s + 180), L((1, 4, 600, 128), s + 181),
+         L((1, 4, 1024, 128), s + 182, "few"), L((1, 4, 200, 128), s + 183)], "mixed")
+    add("fix_size_l2", {"fix_kv_size": 512, "keep_ratio": 0.0, "strategy": "keep_low",
+                        "skip_layers": []}, f, [L((1, 32, 16384, 128), s + 184)], "headline")
 
 
 def run_case(case, positions):
@@ -215,10 +259,10 @@ def run_case(case, positions):
 def gen_prims():
     """Direct fixtures for the torch primitives the oracle restates."""
     meta, arrs = [], {}
-    for dt in ("bf16", "fp32"):
+    for dt in ("bf16", "fp32", "fp16"):
         for D in (64, 80, 128):
             for var in ("normal", "scaled", "special", "few"):
-                seed = 5000 + D + (0 if dt == "bf16" else 7) + 11 * ("normal", "scaled", "special", "few").index(var)
+                seed = 5000 + D + {"bf16": 0, "fp32": 7, "fp16": 3}[dt] + 11 * ("normal", "scaled", "special", "few").index(var)
                 K = prng.gen_keys(seed, (1, 4, 2048, D), dt, var)
                 n = torch.norm(to_torch(K, dt), p=2, dim=-1)
                 nn = to_np(n, dt)
@@ -238,7 +282,49 @@ def gen_prims():
     return meta, arrs
 
 
+def gen_snapkv_prims():
+    """snapkv_lite's scoring tensors (snapkv_lite.py:96-121: norm, max + 1e-6, subtraction,
+    avg_pool1d) evaluated with torch on rows whose maxima sit where the python scalar's dtype
+    cast is visible (bf16 [2e-9, 4e-9), fp16 [1.2e-4, 2.4e-4)) and on ordinary rows."""
+    meta, arrs = [], {}
+    i = 0
+    for dt in ("bf16", "fp16", "fp32"):
+        for var in ("micro", "tiny", "normal", "special"):
+            for pk in (5, 4):
+                seed = 7000 + i
+                i += 1
+                shape = (1, 8, 1000, 80)
+                K = prng.gen_keys(seed, shape, dt, var)
+                n = torch.norm(to_torch(K, dt), p=2, dim=-1)
+                m = n.max(dim=-1, keepdim=True)[0] + 1e-6
+                sc = m - n
+                pooled = torch.nn.functional.avg_pool1d(sc.view(8, 1, 1000), kernel_size=pk,
+                                                        stride=1, padding=pk // 2)[:, :, :1000]
+                key = f"snapkv_{dt}_{var}_pk{pk}"
+                arrs[key + "_max_eps"] = to_np(m, dt)
+                arrs[key + "_scores"] = to_np(sc, dt)
+                arrs[key + "_pooled"] = to_np(pooled.view(1, 8, 1000), dt)
+                meta.append({"key": key, "dtype": dt, "variant": var, "seed": seed,
+                             "shape": list(shape), "pool": pk, "input_sha": sha(K)})
+    return meta, arrs
+
+
+def write_prims(meta):
+    pm, pa = gen_prims()
+    sm, sa = gen_snapkv_prims()
+    with open(os.path.join(HERE, "prims.json"), "w") as f:
+        json.dump({"meta": meta, "prims": pm, "snapkv": sm}, f, indent=1)
+    np.savez_compressed(os.path.join(HERE, "prims.npz"), **pa, **sa)
+    return pm, sm
+
+
 def main():
+    if "--prims-only" in sys.argv:
+        with open(os.path.join(HERE, "cases.json")) as f:
+            meta = json.load(f)["meta"]
+        pm, sm = write_prims(meta)
+        print("wrote", len(pm), "prim sets,", len(sm), "snapkv score sets")
+        return
     build_cases()
     positions = {}
     recs = []
@@ -255,11 +341,9 @@ def main():
     with open(os.path.join(HERE, "cases.json"), "w") as f:
         json.dump({"meta": meta, "cases": recs}, f, indent=1)
     np.savez_compressed(os.path.join(HERE, "positions.npz"), **positions)
-    pm, pa = gen_prims()
-    with open(os.path.join(HERE, "prims.json"), "w") as f:
-        json.dump({"meta": meta, "prims": pm}, f, indent=1)
-    np.savez_compressed(os.path.join(HERE, "prims.npz"), **pa)
-    print("wrote", len(recs), "cases,", len(positions), "position arrays,", len(pm), "prim sets")
+    pm, sm = write_prims(meta)
+    print("wrote", len(recs), "cases,", len(positions), "position arrays,", len(pm), "prim sets,",
+          len(sm), "snapkv score sets")
 
 
 if __name__ == "__main__":

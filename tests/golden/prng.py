@@ -3,9 +3,10 @@
 Fixtures store only a recipe (seed, shape, dtype, variant) plus expected outputs, so the
 inputs must be reproducible bit-for-bit on any IEEE machine: splitmix64 counter stream ->
 53-bit uniforms -> (u0+u1+u2+u3-2)*sqrt(3) in float64 (plain IEEE adds/multiplies, no libm)
--> RNE to float32 -> RNE to bfloat16 (c10::BFloat16 rounding).
+-> RNE to float32 -> RNE to bfloat16 (c10::BFloat16 rounding) or float16 (IEEE RNE, as numpy's
+and c10::Half's conversions both do).
 
-bf16 tensors are represented as numpy uint16 bit patterns.
+bf16 tensors are represented as numpy uint16 bit patterns, fp16 tensors as numpy float16.
 """
 import numpy as np
 
@@ -59,11 +60,14 @@ def to_dtype(x_f32, dtype):
         return f32_to_bf16_bits(x_f32)
     if dtype == "fp32":
         return np.ascontiguousarray(x_f32, dtype=np.float32)
+    if dtype == "fp16":
+        with np.errstate(over="ignore"):
+            return np.ascontiguousarray(x_f32, dtype=np.float32).astype(np.float16)
     raise ValueError(dtype)
 
 
 def gen_keys(seed, shape, dtype, variant="normal"):
-    """K[B,H,S,D] in storage representation (uint16 bits for bf16, float32 for fp32)."""
+    """K[B,H,S,D] in storage representation (uint16 bits for bf16, float16 / float32 otherwise)."""
     B, H, S, D = shape
     n = B * H * S * D
     if variant == "normal":
@@ -90,6 +94,10 @@ def gen_keys(seed, shape, dtype, variant="normal"):
         x = x.reshape(-1)
     elif variant == "tiny":  # norms ~1e-3: the +1e-6 in snapkv_lite becomes visible
         x = (normal_f32(seed, n) * np.float32(1e-4)).astype(np.float32)
+    elif variant == "micro":  # norms at the bottom of the dtype's range, where snapkv_lite's
+        # `max + 1e-6` rounds differently for a dtype-cast and an fp32 epsilon
+        scale = {"bf16": 2.3e-10, "fp32": 2.3e-10, "fp16": 1.1e-5}[dtype]
+        x = (normal_f32(seed, n) * np.float32(scale)).astype(np.float32)
     elif variant == "zero":
         x = np.zeros(n, dtype=np.float32)
     else:
@@ -103,7 +111,7 @@ def gen_values(seed, shape, dtype):
 
 
 def encode_positions(shape, dtype):
-    """V whose rows encode their own (b, h, s): exact in bf16 (ints <= 255) and fp32."""
+    """V whose rows encode their own (b, h, s): exact in bf16 (ints <= 255), fp16 and fp32."""
     B, H, S, D = shape
     assert D >= 4
     v = np.zeros((B, H, S, D), dtype=np.float32)
@@ -118,7 +126,7 @@ def encode_positions(shape, dtype):
 
 def decode_positions(v_out, dtype):
     """Inverse of encode_positions on a [B,H,n,D] array; returns (pos[B,H,n], ok)."""
-    v = bf16_bits_to_f32(v_out) if dtype == "bf16" else np.asarray(v_out, dtype=np.float32)
+    v = bf16_bits_to_f32(v_out) if dtype == "bf16" else np.asarray(v_out).astype(np.float32)
     pos = (v[..., 0].astype(np.int64) * 256 + v[..., 1].astype(np.int64))
     B, H = v.shape[0], v.shape[1]
     ok = bool(np.all(v[..., 2] == np.arange(H)[None, :, None]) and

@@ -4,6 +4,7 @@ import torch
 
 
 def to_dev(a, device="cuda:0"):
+    """uint16 bits -> bfloat16; float16 / float32 map to torch.float16 / torch.float32."""
     a = np.ascontiguousarray(a)
     if a.dtype == np.uint16:
         return torch.from_numpy(a.view(np.int16)).view(torch.bfloat16).to(device)

@@ -77,4 +77,8 @@ extern "C" uint32_t model_key_bf16(uint32_t b, int desc) { return kvc::key_bf16(
 extern "C" uint32_t model_key_f32(uint32_t b, int desc) { return kvc::key_f32(b, desc != 0); }
 extern "C" uint32_t model_f32_to_bf16(float f) { return kvc::f32_to_bf16_rne(f); }
 extern "C" uint32_t model_canon_nan(uint32_t w) { return kvc::canon_nan_bf16x2(w); }
+extern "C" uint32_t model_key_f16(uint32_t b, int desc) { return kvc::key_f16(b, desc != 0); }
+extern "C" uint32_t model_f32_to_f16(float f) { return kvc::f32_to_f16_rne(f); }
+extern "C" float model_f16_to_f32(uint32_t h) { return kvc::f16_to_f32(h); }
+extern "C" uint32_t model_canon_nan_f16(uint32_t w) { return kvc::canon_nan_f16x2(w); }
 

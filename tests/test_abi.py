@@ -67,12 +67,24 @@ def test_plan_fills_prefix_fields_and_layout():
 
 
 @pytest.mark.parametrize("bad, code", [
-    (dict(dtype=5), -2), (dict(head_dim=96), -3), (dict(head_dim=100), -3), (dict(batch=0), -1),
+    (dict(dtype=5), -2), (dict(dtype=3), -2), (dict(dtype=2, head_dim=96), -3),
+    (dict(head_dim=96), -3), (dict(head_dim=100), -3), (dict(batch=0), -1),
     (dict(order=3), -1), (dict(algo=9), -1)])
 def test_plan_rejects_bad_params(bad, code):
     table = np.array([_layer(100, 0, 100, 10)], dtype=N.LAYER_DTYPE)
     rc, _ = N.plan(_params(**bad), table)
     assert rc == code
+
+
+def test_plan_accepts_fp16():
+    """KVC_F16 (transformers-5 pythia caches): 2-byte elements like bf16 in every region."""
+    table = np.array([_layer(16384, 0, 16384, 512)], dtype=N.LAYER_DTYPE)
+    rc16, i16 = N.plan(_params(dtype=N.KVC_F16), table.copy())
+    rcb, ib = N.plan(_params(dtype=N.KVC_BF16), table.copy())
+    assert rc16 == 0 and rcb == 0
+    assert i16.workspace_bytes == ib.workspace_bytes and i16.norm_row_stride == ib.norm_row_stride
+    for hd in (64, 80, 128, 160, 256):  # 128/160/256/320/512-byte rows
+        assert N.plan(_params(dtype=N.KVC_F16, head_dim=hd), table.copy())[0] == 0
 
 
 def test_plan_rejects_bad_layers():

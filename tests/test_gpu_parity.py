@@ -79,7 +79,8 @@ def _abi_select(keys_np, n_select, order, algo, score_mode=0, pool=0, zone=None)
     t["k_stride"] = t["v_stride"] = K.stride()[:3]
     t["seq_len"], t["zone_start"], t["zone_len"], t["n_select"] = S, z0, zl, n_select
     t["score_mode"], t["pool_kernel"] = score_mode, pool
-    p = N.Params(dtype=N.KVC_BF16 if K.dtype == torch.bfloat16 else N.KVC_F32, batch=B, heads=H,
+    dts = {torch.bfloat16: N.KVC_BF16, torch.float16: N.KVC_F16, torch.float32: N.KVC_F32}
+    p = N.Params(dtype=dts[K.dtype], batch=B, heads=H,
                  head_dim=D, order=order, algo=algo, phases=N.PHASE_SCORE | N.PHASE_SELECT,
                  external_index=0)
     rc, info = N.plan(p, table)
@@ -98,9 +99,9 @@ def _abi_select(keys_np, n_select, order, algo, score_mode=0, pool=0, zone=None)
     return to_np(nr).reshape(B, H, zl), ir[:, :n_select].cpu().numpy().reshape(B, H, n_select)
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("dtype", ["bf16", "fp16", "fp32"])
 @pytest.mark.parametrize("D", [64, 80, 128])
-@pytest.mark.parametrize("variant", ["normal", "scaled", "few", "equal", "special", "tiny"])
+@pytest.mark.parametrize("variant", ["normal", "scaled", "few", "equal", "special", "tiny", "micro"])
 def test_abi_norms_and_sort_select(dtype, D, variant):
     S = 3000
     K = prng.gen_keys(900 + D, (1, 4, S, D), dtype, variant)
@@ -112,7 +113,7 @@ def test_abi_norms_and_sort_select(dtype, D, variant):
             np.testing.assert_array_equal(idx, ref, err_msg=f"sort k={k} desc={desc}")
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("dtype", ["bf16", "fp16", "fp32"])
 @pytest.mark.parametrize("variant", ["normal", "few", "equal", "special"])
 def test_abi_topk_select(dtype, variant):
     S = 4000
@@ -230,7 +231,7 @@ def test_more_layers_than_one_argument_chunk(launch_path):
         assert np.array_equal(to_np(ko), rk) and np.array_equal(to_np(vo), rv), li
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("dtype", ["bf16", "fp16", "fp32"])
 def test_zones_longer_than_lds_limit(dtype):
     """Zones > 16384 positions select from the global-scratch variant (up to 65536; the
     cross-wave counts of segments > 32767 positions use the packed counters' top bit)."""

@@ -50,7 +50,7 @@ def _prim_inputs(p):
     return K
 
 
-@pytest.mark.parametrize("idx", range(24))
+@pytest.mark.parametrize("idx", range(len(fixtures.prims()[0]["prims"])))
 def test_oracle_primitives_match_torch_golden(idx):
     meta, arrs = fixtures.prims()
     p = meta["prims"][idx]
@@ -63,3 +63,24 @@ def test_oracle_primitives_match_torch_golden(idx):
                                   arrs[p["key"] + "_argsort_desc"])
     for k in p["topk_ks"]:
         np.testing.assert_array_equal(oracle.topk_indices(n, k), arrs[f"{p['key']}_topk{k}"])
+
+
+@pytest.mark.parametrize("idx", range(len(fixtures.prims()[0]["snapkv"])))
+def test_oracle_snapkv_scores_match_torch_golden(idx):
+    """snapkv_lite scoring (snapkv_lite.py:96-121) bit-for-bit, incl. rows whose maxima sit where
+    `max + 1e-6` differs between an fp32 epsilon and the dtype-cast python scalar torch uses."""
+    meta, arrs = fixtures.prims()
+    p = meta["snapkv"][idx]
+    K = _prim_inputs(p)
+    n = oracle.norms(K)
+
+    def bits(a):
+        # exact bits, except that every NaN is one value: torch's vectorised bf16 ops emit NaN
+        # as 0xFFFF where a scalar conversion gives 0x7FC0, and the sort keys treat all NaNs as
+        # one key, so NaN payloads never reach the selection
+        f = a.astype(np.float32) if a.dtype != np.uint16 else prng.bf16_bits_to_f32(a)
+        b = a.view(np.uint16).astype(np.int64) if a.dtype != np.float32 else a.view(np.uint32).astype(np.int64)
+        return np.where(np.isnan(f), -1, b)
+    np.testing.assert_array_equal(bits(oracle.snapkv_scores(n, 1)), bits(arrs[p["key"] + "_scores"]))
+    np.testing.assert_array_equal(bits(oracle.snapkv_scores(n, p["pool"])),
+                                  bits(arrs[p["key"] + "_pooled"]))

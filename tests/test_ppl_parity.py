@@ -69,7 +69,7 @@ def test_harness_runs_with_oracle_on_cpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("name,kw", CASES)
 def test_ppl_delta_zero_engine_vs_oracle(dtype, name, kw):
     from kvcompress.evaluate import evaluate_with_compression

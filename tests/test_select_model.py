@@ -36,6 +36,14 @@ def model():
         getattr(L, f).argtypes = [ctypes.c_uint32, ctypes.c_int] if "key" in f else [ctypes.c_uint32]
     L.model_f32_to_bf16.restype = ctypes.c_uint32
     L.model_f32_to_bf16.argtypes = [ctypes.c_float]
+    L.model_key_f16.restype = ctypes.c_uint32
+    L.model_key_f16.argtypes = [ctypes.c_uint32, ctypes.c_int]
+    L.model_f32_to_f16.restype = ctypes.c_uint32
+    L.model_f32_to_f16.argtypes = [ctypes.c_float]
+    L.model_f16_to_f32.restype = ctypes.c_float
+    L.model_f16_to_f32.argtypes = [ctypes.c_uint32]
+    L.model_canon_nan_f16.restype = ctypes.c_uint32
+    L.model_canon_nan_f16.argtypes = [ctypes.c_uint32]
     return L
 
 
@@ -132,3 +140,37 @@ def test_bf16_rounding_and_nan_canonicalisation(model):
             return 0xFFFF if (h & 0x7FFF) > 0x7F80 else h
         assert model.model_canon_nan(w) == (c(lo) | (c(hi) << 16))
 
+
+
+def test_fp16_keys_conversions_and_nan_quieting(model):
+    """The kernel's fp16 helpers (csrc/kvc_common.h) vs numpy/IEEE: sort-key order equals torch's
+    comparators on all 65536 patterns, f16 -> f32 exact, f32 -> f16 round-to-nearest-even at
+    every fp16 midpoint (incl. subnormals and overflow), gather's NaN quieting (0x7C01 -> 0x7E01)."""
+    allh = np.arange(65536, dtype=np.uint32)
+    f = allh.astype(np.uint16).view(np.float16).astype(np.float32)
+    got = np.array([model.model_f16_to_f32(int(h)) for h in allh], dtype=np.float32)
+    same = (got.view(np.uint32) == f.view(np.uint32)) | (np.isnan(got) & np.isnan(f))
+    assert same.all()
+    rng = np.random.default_rng(4)
+    for desc in (0, 1):
+        kh = np.array([model.model_key_f16(int(b), desc) for b in allh], dtype=np.uint32)
+        a, b = rng.integers(0, 65536, 200000), rng.integers(0, 65536, 200000)
+        np.testing.assert_array_equal(kh[a] < kh[b], _torch_less(f[a], f[b], desc))
+        np.testing.assert_array_equal(kh[a] == kh[b], ~_torch_less(f[a], f[b], desc) & ~_torch_less(f[b], f[a], desc))
+    fin = allh[:0x7C00].astype(np.uint16).view(np.float16).astype(np.float64)
+    mid = ((fin[:-1] + fin[1:]) / 2).astype(np.float32)  # exact midpoints (fp32 has the bits)
+    x = np.concatenate([mid, -mid, np.nextafter(mid, np.float32(np.inf)), np.nextafter(mid, np.float32(0)),
+                        rng.standard_normal(20000).astype(np.float32) * 1e-6,
+                        np.array([np.inf, -np.inf, 0.0, -0.0, 65504, 65519.996, 65520, 1e9, 2.98e-8,
+                                  2.9802322e-8, 1e-40], np.float32)])
+    with np.errstate(over="ignore"):
+        ref = x.astype(np.float16).view(np.uint16)
+    out = np.array([model.model_f32_to_f16(float(v)) for v in x], dtype=np.uint16)
+    np.testing.assert_array_equal(out, ref)
+    assert model.model_f32_to_f16(float("nan")) == 0x7E00
+    for w in (0x7C017C00, 0xFC01FE00, 0x7DFF3C00, 0x12345678, 0xFFFF7FFF):
+        lo, hi = w & 0xFFFF, w >> 16
+
+        def q(h):
+            return h | 0x200 if (h & 0x7FFF) > 0x7C00 else h
+        assert model.model_canon_nan_f16(w) == (q(lo) | (q(hi) << 16))
