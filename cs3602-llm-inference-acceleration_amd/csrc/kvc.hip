@@ -190,15 +190,19 @@ __device__ __forceinline__ void accum_chunk(float (&acc)[8], const uint4 x, int 
   }
 }
 
+// 16-B chunks of a token row staged per phase: 4 (64-B rows), 8 (multiples of 128 B), 10 (160 B
+// multiples); a row of NC chunks takes NC / CP phases.
+__host__ __device__ constexpr int score_cp(int nc) { return nc == 4 ? 4 : (nc % 8 == 0 ? 8 : 10); }
+
 // One 64-token tile of one (layer, b, h) row: coalesced 16-B loads -> per-wave LDS slab ->
-// one lane per token, torch.norm's 8-accumulator FMA order (fp16: its serial order).  `wl` is this wave's slab
-// (kTile * ROWB bytes).  sc1 = publish the norms write-through for an in-launch consumer.
+// one lane per token, torch.norm's 8-accumulator FMA order (fp16: its serial order).  `wl` is
+// this wave's slab (kTile * ROWB bytes).  sc1 = publish the norms write-through for an in-launch consumer.
 template <int DT, int NC, bool NTL = false>
 __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int tt, int H,
                                            char* wl, char* norms, int64_t norm_stride,
                                            bool sc1) {
   constexpr int ESZ = DTypeTraits<DT>::esz;
-  constexpr int CP = (NC % 8 == 0) ? 8 : 10;  // 16-B chunks per token per phase
+  constexpr int CP = score_cp(NC);  // 16-B chunks per token per phase
   constexpr int NPH = NC / CP;
   constexpr int ROWB = CP * 16 + 16;  // padded LDS row: conflict-free ds_read_b128 per lane
   const int lane = threadIdx.x & 63;
@@ -272,27 +276,29 @@ template <int DT, int NC, bool NTL>
 __global__ void __launch_bounds__(kScoreThreads)
     score_kernel(const LayerChunk T, int nl, int H, int64_t tile_base, int64_t chunk_tiles,
                  char* __restrict__ norms, int64_t norm_stride) {
-  constexpr int CP = (NC % 8 == 0) ? 8 : 10;
+  constexpr int CP = score_cp(NC);
   constexpr int ROWB = CP * 16 + 16;
   __shared__ __attribute__((aligned(16))) char lds[kScoreWaves][kTile * ROWB];
   const kvc_layer_t* L = T.l;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t gl = (int64_t)blockIdx.x * kScoreWaves + wid;
-  if (gl >= chunk_tiles) return;
-  const int64_t g = tile_base + gl;  // global tile index (kvc_plan's tile0 numbering)
-  int lo = 0, hi = nl - 1;  // largest layer with tile0 <= g
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (L[mid].tile0 <= g)
-      lo = mid;
-    else
-      hi = mid - 1;
+  // one tile per wave (default grid); a smaller grid makes the waves stride over the tiles
+  const int64_t stride = (int64_t)gridDim.x * kScoreWaves;
+  for (int64_t gl = (int64_t)blockIdx.x * kScoreWaves + wid; gl < chunk_tiles; gl += stride) {
+    const int64_t g = tile_base + gl;  // global tile index (kvc_plan's tile0 numbering)
+    int lo = 0, hi = nl - 1;  // largest layer with tile0 <= g
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (L[mid].tile0 <= g)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    const kvc_layer_t* ly = L + lo;
+    const int tpr = (ly->zone_len + kTile - 1) / kTile;
+    const int local = (int)(g - ly->tile0);
+    const int row = local / tpr;
+    score_tile<DT, NC, NTL>(ly, row, local - row * tpr, H, lds[wid], norms, norm_stride, false);
   }
-  const kvc_layer_t* ly = L + lo;
-  const int tpr = (ly->zone_len + kTile - 1) / kTile;
-  const int local = (int)(g - ly->tile0);
-  const int row = local / tpr;
-  score_tile<DT, NC, NTL>(ly, row, local - row * tpr, H, lds[wid], norms, norm_stride, false);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1275,7 +1281,9 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
   const int rowb = p->head_dim * es;
   if (rowb % 16) return KVC_E_HEADDIM;
   const int nc = rowb / 16;
-  if (nc != 8 && nc != 10 && nc != 16 && nc != 20 && nc != 32) return KVC_E_HEADDIM;
+  // 64..1024-byte rows: every pythia geometry (D 32/64/80/128/256) in bf16, fp16 and fp32
+  if (nc != 4 && nc != 8 && nc != 10 && nc != 16 && nc != 20 && nc != 32 && nc != 64)
+    return KVC_E_HEADDIM;
   const int64_t BH = (int64_t)p->batch * p->heads;
   if (BH * nl > 0x7FFFFFFF) return KVC_E_ARG;
   int64_t tiles = 0, units = 0, max_zone = 0, max_sel = 0;
@@ -1347,7 +1355,10 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
 template <int DT, int NC>
 static void launch_score(const LayerChunk& T, int nl, int H, int64_t tile_base,
                          int64_t chunk_tiles, char* norms, int64_t nstride, hipStream_t s) {
-  const unsigned grid = (unsigned)((chunk_tiles + kScoreWaves - 1) / kScoreWaves);
+  unsigned grid = (unsigned)((chunk_tiles + kScoreWaves - 1) / kScoreWaves);
+  // tuning only: a persistent grid of KVC_SCORE_GRID workgroups (waves stride over the tiles)
+  if (const char* e = getenv("KVC_SCORE_GRID"))
+    if (atoi(e) > 0 && (unsigned)atoi(e) < grid) grid = (unsigned)atoi(e);
   const char* ntl = getenv("KVC_SCORE_NT");  // keys are read once: non-temporal by default
   if (!(ntl && strcmp(ntl, "0") == 0))
     hipLaunchKernelGGL((score_kernel<DT, NC, true>), dim3(grid), dim3(kScoreThreads), 0, s, T,
@@ -1383,11 +1394,13 @@ static void dispatch_nc(int nc, bool score, const LayerChunk& T, int nl, int H, 
       launch_gather<DT, NCV>(T, nl, H, BH, idx, istride, work, s);         \
     break;
   switch (nc) {
+    KVC_NC_CASE(4)
     KVC_NC_CASE(8)
     KVC_NC_CASE(10)
     KVC_NC_CASE(16)
     KVC_NC_CASE(20)
     KVC_NC_CASE(32)
+    KVC_NC_CASE(64)
     default:
       break;
   }
@@ -1405,11 +1418,13 @@ static void launch_select_gather(int nc, const LayerChunk& T, int nl, int H, int
                        order, algo, norms, nstride, wave_seg, n_cap, cap);                  \
     break;
   switch (nc) {
+    KVC_SG_CASE(4)
     KVC_SG_CASE(8)
     KVC_SG_CASE(10)
     KVC_SG_CASE(16)
     KVC_SG_CASE(20)
     KVC_SG_CASE(32)
+    KVC_SG_CASE(64)
     default:
       break;
   }

@@ -221,6 +221,18 @@ def build_cases():
          L((1, 4, 1024, 128), s + 182, "few"), L((1, 4, 200, 128), s + 183)], "mixed")
     add("fix_size_l2", {"fix_kv_size": 512, "keep_ratio": 0.0, "strategy": "keep_low",
                         "skip_layers": []}, f, [L((1, 32, 16384, 128), s + 184)], "headline")
+    # ---- the rest of the pythia family's head dims: D = 32 (14m/31m), D = 256 (1b) ----
+    for dt in ("bf16", "fp16", "fp32"):
+        for D in (32, 256):
+            add("fix_size_l2", {"fix_kv_size": 256, "keep_ratio": 0.5, "strategy": "keep_low"},
+                dt, [L((1, 4, 700, D), s + 190 + D), L((2, 3, 1500, D), s + 191 + D, "few"),
+                     L((1, 4, 900, D), s + 192 + D, "special")], f"D{D}")
+            add("snapkv_lite", {"observation_window": 32, "keep_size": 512, "pooling_kernel": 5},
+                dt, [L((1, 4, 2048, D), s + 193 + D), L((1, 4, 1500, D), s + 194 + D, "few")],
+                f"D{D}")
+            add("h2o_l2", {"start_size": 4, "heavy_hitter_size": 64, "recent_size": 444}, dt,
+                [L((1, 4, 2048, D), s + 195 + D), L((1, 4, 513, D), s + 196 + D, "scaled")],
+                f"D{D}")
 
 
 def run_case(case, positions):

@@ -83,8 +83,17 @@ def test_plan_accepts_fp16():
     rcb, ib = N.plan(_params(dtype=N.KVC_BF16), table.copy())
     assert rc16 == 0 and rcb == 0
     assert i16.workspace_bytes == ib.workspace_bytes and i16.norm_row_stride == ib.norm_row_stride
-    for hd in (64, 80, 128, 160, 256):  # 128/160/256/320/512-byte rows
+    for hd in (32, 64, 80, 128, 160, 256):  # 64/128/160/256/320/512-byte rows
         assert N.plan(_params(dtype=N.KVC_F16, head_dim=hd), table.copy())[0] == 0
+
+
+def test_plan_accepts_every_pythia_head_dim():
+    """D = 32 (pythia-14m/31m), 64, 80, 128, 256 (pythia-1b) in every dtype: 64..1024-byte rows."""
+    table = np.array([_layer(4096, 0, 4096, 512)], dtype=N.LAYER_DTYPE)
+    for dt in (N.KVC_BF16, N.KVC_F16, N.KVC_F32):
+        for hd in (32, 64, 80, 128, 256):
+            assert N.plan(_params(dtype=dt, head_dim=hd), table.copy())[0] == 0, (dt, hd)
+    assert N.plan(_params(dtype=N.KVC_F32, head_dim=512), table.copy())[0] == -3
 
 
 def test_plan_rejects_bad_layers():

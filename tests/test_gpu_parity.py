@@ -100,7 +100,7 @@ def _abi_select(keys_np, n_select, order, algo, score_mode=0, pool=0, zone=None)
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp16", "fp32"])
-@pytest.mark.parametrize("D", [64, 80, 128])
+@pytest.mark.parametrize("D", [32, 64, 80, 128, 256])
 @pytest.mark.parametrize("variant", ["normal", "scaled", "few", "equal", "special", "tiny", "micro"])
 def test_abi_norms_and_sort_select(dtype, D, variant):
     S = 3000
