@@ -98,7 +98,10 @@ def pmc_traffic(kernel="kvc::score_kernel<1, 16, true>"):
         return None
 
 
-def cpu_baseline(seq_len=S, head_dim=D, seconds=12.0):
+DTYPES = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
+
+
+def cpu_baseline(seq_len=S, head_dim=D, seconds=12.0, dtype="bf16"):
     """The reference's CPU op sequence (oracle/torch_port.py) on this host's cores, bounded."""
     from oracle.torch_port import fix_size_l2_layer
     # the GPU box exposes the whole machine's CPUs but grants one GPU a 16-core share
@@ -106,8 +109,8 @@ def cpu_baseline(seq_len=S, head_dim=D, seconds=12.0):
     threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
     torch.set_num_threads(threads)
     g = torch.Generator().manual_seed(0)
-    k = torch.randn(B, H, seq_len, head_dim, generator=g).to(torch.bfloat16)
-    v = torch.randn(B, H, seq_len, head_dim, generator=g).to(torch.bfloat16)
+    k = torch.randn(B, H, seq_len, head_dim, generator=g).to(DTYPES[dtype])
+    v = torch.randn(B, H, seq_len, head_dim, generator=g).to(DTYPES[dtype])
     fix_size_l2_layer(k, v, FIX)  # warm
     n, t0 = 0, time.perf_counter()
     while time.perf_counter() - t0 < seconds:
@@ -115,7 +118,7 @@ def cpu_baseline(seq_len=S, head_dim=D, seconds=12.0):
         n += 1
     dt = time.perf_counter() - t0
     return {"value": n * seq_len / dt, "unit": "KV tokens/s", "cores": threads, "kind": "port",
-            "sample": f"{n} layers of fix_size_l2(512) on one [1,32,{seq_len},{head_dim}] bf16 "
+            "sample": f"{n} layers of fix_size_l2(512) on one [1,32,{seq_len},{head_dim}] {dtype} "
                       f"layer (torch CPU ops: norm->argsort->sort->gather), {dt:.1f}s, "
                       f"{torch.backends.cpu.get_cpu_capability()}"}
 
@@ -224,6 +227,8 @@ def main():
     ap.add_argument("--layers-total", type=int, default=0,
                     help="shard this many layers over the ranks (strong scaling); "
                          "default: 32 layers per GPU (weak scaling)")
+    ap.add_argument("--dtype", default="bf16", choices=sorted(DTYPES),
+                    help="K/V storage dtype (fp16: what transformers >= 5 loads pythia as)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -255,15 +260,16 @@ def main():
     layers = []
     for _ in range(n_layers):
         k = torch.randn(B, H, seq_len, head_dim, device=dev, generator=g,
-                        dtype=torch.float32).to(torch.bfloat16)
+                        dtype=torch.float32).to(DTYPES[args.dtype])
         v = torch.randn(B, H, seq_len, head_dim, device=dev, generator=g,
-                        dtype=torch.float32).to(torch.bfloat16)
+                        dtype=torch.float32).to(DTYPES[args.dtype])
         layers.append((k, v))
 
     def step():
         return fn(layers, skip_layers=[], **kwargs, **extra)
 
-    nbytes = job_bytes(capture_jobs(step), 2)
+    es = layers[0][0].element_size() if layers else 2
+    nbytes = job_bytes(capture_jobs(step), es)
     # per-kernel durations: the engine splits each launch into its three kernels with HIP
     # events (recorded on the stream they run on) for the whole timed region
     timer = _engine.PhaseTimer()
@@ -284,7 +290,7 @@ def main():
         kern = max(dur, key=dur.get)  # dominant kernel of the step
         kern_gbps = nbytes[kern] / (dur[kern] * 1e-3) / 1e9
         headline = args.workload == HEADLINE
-        traffic = pmc_traffic() if headline and kern == "score" else None
+        traffic = pmc_traffic() if headline and kern == "score" and args.dtype == "bf16" else None
         path_gbps = nbytes["path"] * world / (ms_step * 1e-3) / 1e9
         desc = {"score": "score_kernel (key L2 norms)",
                 "select+gather": "select_gather_kernel (selection + segment copy)"}[kern]
@@ -300,7 +306,7 @@ def main():
             "higher_is_better": True,
             "scaling": scaling,
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": args.dtype,
             "data": "synthetic (torch.randn, HBM-resident)",
             "config": {"workload": f"{method}_compress({cfg_kw}, skip_layers=[]) over "
                                    f"{n_layers} layers of K,V [1,{H},{seq_len},{head_dim}] per "
@@ -323,7 +329,7 @@ def main():
         ev = sum(kv[0].size(2) for kv in layers) - sum(kv[0].size(2) for kv in step())
         res["tokens_evicted_per_sec"] = ev * world * args.steps / elapsed
         if not args.no_cpu_baseline and method == "fix_size_l2":
-            res["cpu_baseline"] = cpu_baseline(seq_len, head_dim)
+            res["cpu_baseline"] = cpu_baseline(seq_len, head_dim, dtype=args.dtype)
             res["ppl_delta_vs_ref"] = ppl_delta(dev)
         print(json.dumps(res), flush=True)
     if dist:

@@ -18,17 +18,19 @@ from kvcompress.methods import get_compress_fn  # noqa: E402
 S = int(sys.argv[1]) if len(sys.argv) > 1 else 513
 method = sys.argv[2] if len(sys.argv) > 2 else "fix_size_l2"
 kw = json.loads(sys.argv[3]) if len(sys.argv) > 3 else {"fix_kv_size": 512}
+dt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[
+    os.environ.get("HOST_PROFILE_DTYPE", "bf16")]
+n = int(os.environ.get("HOST_PROFILE_CALLS", "200"))
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(0)
-layers = [(torch.randn(1, 32, S, 128, device=dev, generator=g).to(torch.bfloat16),
-           torch.randn(1, 32, S, 128, device=dev, generator=g).to(torch.bfloat16))
+layers = [(torch.randn(1, 32, S, 128, device=dev, generator=g).to(dt),
+           torch.randn(1, 32, S, 128, device=dev, generator=g).to(dt))
           for _ in range(32)]
 fn = get_compress_fn(method)
 call = lambda: fn(layers, skip_layers=[], **kw)  # noqa: E731
 for _ in range(20):
     call()
 torch.cuda.synchronize()
-n = 200
 t0 = time.perf_counter()
 for _ in range(n):
     call()
@@ -55,7 +57,7 @@ pr.disable()
 torch.cuda.synchronize()
 buf = io.StringIO()
 pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(18)
-print(json.dumps({"S": S, "method": method, "ms_per_call_synced": synced,
+print(json.dumps({"S": S, "method": method, "dtype": str(dt), "ms_per_call_synced": synced,
                   "ms_per_call_issue_only": issue, "ms_per_call_pipelined": drained,
                   "ms_per_call_events": gpu}))
 print(buf.getvalue())
