@@ -39,6 +39,7 @@ class Segments:
 
 
 _SUPPORTED = {torch.bfloat16: N.KVC_BF16, torch.float16: N.KVC_F16, torch.float32: N.KVC_F32}
+_ESIZE = {torch.bfloat16: 2, torch.float16: 2, torch.float32: 4}
 
 
 class PhaseTimer:
@@ -75,19 +76,23 @@ def set_phase_timer(t):
 
 
 def _check_tensors(j: Segments):
+    """Device / dtype / shape contract of a layer that needs the engine; returns K's shape."""
     k, v = j.keys, j.values
     if not (k.is_cuda and v.is_cuda):
         raise RuntimeError(
             f"kvcompress (MI355X HIP engine): layer {j.layer_idx} needs compression but its K/V "
             f"are on {k.device}/{v.device}; this engine runs on ROCm GPU tensors only "
             "(no CPU fallback).")
-    if k.dtype not in _SUPPORTED or v.dtype != k.dtype:
+    kd = k.dtype
+    if kd not in _SUPPORTED or v.dtype != kd:
         raise TypeError(
             f"kvcompress (MI355X HIP engine) supports bfloat16/float16/float32 K and V of one dtype; "
-            f"layer {j.layer_idx} has {k.dtype}/{v.dtype}")
-    if k.dim() != 4 or v.shape != k.shape:
+            f"layer {j.layer_idx} has {kd}/{v.dtype}")
+    shape = k.shape
+    if len(shape) != 4 or v.shape != shape:
         raise ValueError(f"layer {j.layer_idx}: K/V must both be [B, H, S, D]; got "
-                         f"{tuple(k.shape)} / {tuple(v.shape)}")
+                         f"{tuple(shape)} / {tuple(v.shape)}")
+    return shape
 
 
 def _prep(t):
@@ -105,9 +110,8 @@ def execute(jobs: List[Segments], out_list: list, order: int, algo: int):
         return
     groups = {}
     for j in jobs:
-        _check_tensors(j)
-        B, H, S, D = j.keys.shape
-        groups.setdefault((j.keys.device, j.keys.dtype, B, H, D), []).append(j)
+        B, H, _, D = _check_tensors(j)
+        groups.setdefault((j.keys.get_device(), j.keys.dtype, B, H, D), []).append(j)
     for (device, dtype, B, H, D), js in groups.items():
         _run_group(device, dtype, B, H, D, js, out_list, order, algo)
 
@@ -156,28 +160,42 @@ def _run_group(device, dtype, B, H, D, js, out_list, order, algo):
     external = any(j.ext_index is not None for j in js)
     if external and not all(j.ext_index is not None or j.n_select == 0 for j in js):
         raise RuntimeError("mixed external / engine-selected layers in one group")
-    table = np.zeros(n, dtype=N.LAYER_DTYPE)
-    ks = [_prep(j.keys) for j in js]  # prepared inputs stay alive until enqueued
-    vs = [_prep(j.values) for j in js]
+    es = _ESIZE[dtype]
+    rows_ok = (D * es) % 16 == 0
     n_outs = [j.sink_len + j.n_select + j.tail_len for j in js]
     if all(x == n_outs[0] for x in n_outs):
         # one allocation for every output of the call (decode steps: 64 tensors per token);
         # each layer's K / V is a disjoint contiguous view of it
-        o = torch.empty((2 * n, B, H, n_outs[0], D), dtype=dtype, device=device).unbind(0)
+        buf = torch.empty((2 * n, B, H, n_outs[0], D), dtype=dtype, device=device)
+        o = buf.unbind(0)
         kos, vos = o[:n], o[n:]
+        base, step = buf.data_ptr(), B * H * n_outs[0] * D * es
+        kops = [base + i * step for i in range(n)]
+        vops = [base + (n + i) * step for i in range(n)]
     else:
         kos = [torch.empty((B, H, x, D), dtype=dtype, device=device) for x in n_outs]
         vos = [torch.empty((B, H, x, D), dtype=dtype, device=device) for x in n_outs]
-    table["k"] = [t.data_ptr() for t in ks]
-    table["v"] = [t.data_ptr() for t in vs]
-    table["k_out"] = [t.data_ptr() for t in kos]
-    table["v_out"] = [t.data_ptr() for t in vos]
-    table["k_stride"] = [t.stride()[:3] for t in ks]
-    table["v_stride"] = [t.stride()[:3] for t in vs]
-    table["seq_len"] = [t.shape[2] for t in ks]
-    for f in ("zone_start", "zone_len", "n_select", "sink_len", "tail_start", "tail_len",
-              "pool_kernel", "score_mode"):
-        table[f] = [getattr(j, f) for j in js]
+        kops = [t.data_ptr() for t in kos]
+        vops = [t.data_ptr() for t in vos]
+    # one pass per layer: pointers, strides, segment bounds (inputs that are not plain
+    # contiguous 16-B aligned rows go through _prep; prepared copies stay alive in `keep`)
+    rows, keep = [], []
+    for i, j in enumerate(js):
+        k, v = j.keys, j.values
+        kp, vp = k.data_ptr(), v.data_ptr()
+        if not (rows_ok and kp % 16 == 0 and k.is_contiguous()):
+            k = _prep(k)
+            kp = k.data_ptr()
+            keep.append(k)
+        if not (rows_ok and vp % 16 == 0 and v.is_contiguous()):
+            v = _prep(v)
+            vp = v.data_ptr()
+            keep.append(v)
+        kst, vst = k.stride(), v.stride()
+        rows.append((kp, vp, kops[i], vops[i], kst[:3], vst[:3], k.shape[2], j.zone_start,
+                     j.zone_len, j.n_select, j.sink_len, j.tail_start, j.tail_len,
+                     j.pool_kernel, j.score_mode, 0, 0, 0, 0))
+    table = np.array(rows, dtype=N.LAYER_DTYPE)
 
     def params():
         return N.Params(dtype=_SUPPORTED[dtype], batch=B, heads=H, head_dim=D, order=order,
