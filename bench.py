@@ -112,15 +112,30 @@ def cpu_baseline(seq_len=S, head_dim=D, seconds=12.0, dtype="bf16"):
     k = torch.randn(B, H, seq_len, head_dim, generator=g).to(DTYPES[dtype])
     v = torch.randn(B, H, seq_len, head_dim, generator=g).to(DTYPES[dtype])
     fix_size_l2_layer(k, v, FIX)  # warm
-    n, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        fix_size_l2_layer(k, v, FIX)
-        n += 1
-    dt = time.perf_counter() - t0
+
+    def rate(secs):
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < secs:
+            fix_size_l2_layer(k, v, FIX)
+            n += 1
+        return n, time.perf_counter() - t0
+
+    n, dt = rate(seconds)
+    torch.set_num_threads(1)  # also a 1-thread run
+    n1, dt1 = rate(seconds / 3)
+    torch.set_num_threads(threads)
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
     return {"value": n * seq_len / dt, "unit": "KV tokens/s", "cores": threads, "kind": "port",
+            "value_1_thread": n1 * seq_len / dt1, "cpu_model": model,
+            "cpu_capability": torch.backends.cpu.get_cpu_capability(),
             "sample": f"{n} layers of fix_size_l2(512) on one [1,32,{seq_len},{head_dim}] {dtype} "
-                      f"layer (torch CPU ops: norm->argsort->sort->gather), {dt:.1f}s, "
-                      f"{torch.backends.cpu.get_cpu_capability()}"}
+                      f"layer (torch CPU ops: norm->argsort->sort->gather) in {dt:.1f}s on "
+                      f"{threads} threads, {n1} layers in {dt1:.1f}s on 1 thread"}
 
 
 def ppl_delta(device, tokens=256, fix=64, keep_ratio=0.5):
