@@ -36,7 +36,8 @@ constexpr int kSelWaves = kSelThreads / 64;
 constexpr int kSelThreadsSmall = 256;  // select workgroup for zones of up to kSmallZone
 constexpr int kSmallZone = kSelThreadsSmall * 16;
 constexpr int kZoneMax = 16384;        // longest zone whose selection runs from LDS
-constexpr int kZoneMaxGlobal = 65536;  // longest zone at all (u16 positions; global scratch)
+constexpr int kZoneMaxGlobal = 65536;  // longest zone of the u16-position global variant
+constexpr int kZoneMaxLong = 1 << 24;   // longest zone at all (u32 positions; global scratch)
 constexpr int kWaveSeg = 128;    // default: segments this short are finished by one wave
 constexpr int kGatherThreads = 256;
 constexpr int kGatherTokens = 64;  // output tokens per gather block
@@ -918,6 +919,215 @@ __global__ void __launch_bounds__(kSelThreads)
       n_cap, n_cap / 2 + 1, sc, wave_seg, nullptr);
 }
 
+// Zones longer than kZoneMaxGlobal (up to kZoneMaxLong): the same partition chain with u32
+// positions and full rank tables in a per-row global scratch
+//   key[n_cap] | idx[n_cap] (u32) | spos[n_cap/2 + 2] (u32) | gpos[n_cap/2 + 2] (u32)
+// Too many positions per lane to keep a level's flags in registers, so each pass re-derives
+// them from the keys (the keys do not change between a level's passes: the median move and the
+// swaps run after the last one); counts are plain ints.  Rare, long rows: simplicity over speed.
+__host__ __device__ constexpr size_t sel_long_bytes(int n_cap, int key_size) {
+  return (size_t)n_cap * key_size + (size_t)n_cap * 4 + 2 * (size_t)(n_cap / 2 + 2) * 4;
+}
+
+struct LongScalars {
+  int ge[kSelWaves];
+  int le[kSelWaves];
+  int nsw[kSelWaves];
+  int ff[kSelWaves];
+};
+
+// One level over [lo, hi) (see run_chain for the algorithm); returns cut.
+template <typename KeyT>
+__device__ int partition_long(KeyT* key, uint32_t* idx, uint32_t* spos, uint32_t* gpos,
+                              LongScalars& sc, int lo, int hi) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6);
+  const int a = lo + 1, b = lo + (hi - lo) / 2, c = hi - 1;
+  const uint32_t ka = (uint32_t)uni((int)key[a]), kb = (uint32_t)uni((int)key[b]);
+  const uint32_t kc = (uint32_t)uni((int)key[c]), klo = (uint32_t)uni((int)key[lo]);
+  int ch;  // std::__move_median_to_first(lo, a, b, c)
+  if (ka < kb) {
+    if (kb < kc) ch = b; else if (ka < kc) ch = c; else ch = a;
+  } else if (ka < kc) {
+    ch = a;
+  } else if (kb < kc) {
+    ch = c;
+  } else {
+    ch = b;
+  }
+  const uint32_t p = (ch == a) ? ka : (ch == b) ? kb : kc;
+  const int J = (hi - lo - 1 + kSelThreads - 1) / kSelThreads;
+  const int wbeg = lo + 1 + wid * J * 64;
+  const int half = (hi - lo) / 2 + 1;  // swapped ranks m <= (n - 1) / 2
+  // ---- P1: wave counts of ge / le positions ----
+  int cge = 0, cle = 0;
+  for (int j = 0; j < J; ++j) {
+    const int pos = wbeg + j * 64 + lane;
+    const bool inb = pos < hi;
+    const uint32_t kk = inb ? (pos == ch ? klo : (uint32_t)key[pos]) : 0u;
+    cge += __popcll(__builtin_amdgcn_ballot_w64(inb && kk >= p));
+    cle += __popcll(__builtin_amdgcn_ballot_w64(inb && kk <= p));
+  }
+  if (lane == 0) {
+    sc.ge[wid] = cge;
+    sc.le[wid] = cle;
+  }
+  __syncthreads();
+  int ge_before = 0, le_before = 0, tot_le = 0;
+  for (int w = 0; w < kSelWaves; ++w) {
+    const int g = sc.ge[w], l = sc.le[w];
+    ge_before += w < wid ? g : 0;
+    le_before += w < wid ? l : 0;
+    tot_le += l;
+  }
+  // ---- P2: rank -> position tables, swap count, first unswapped ge ----
+  int rge = ge_before, rle = le_before, nsw = 0, ff = kBig;
+  for (int j = 0; j < J; ++j) {
+    const int pos = wbeg + j * 64 + lane;
+    const bool inb = pos < hi;
+    const uint32_t kk = inb ? (pos == ch ? klo : (uint32_t)key[pos]) : 0u;
+    const bool ge = inb && kk >= p, le = inb && kk <= p;
+    const uint64_t bg = __builtin_amdgcn_ballot_w64(ge), bl = __builtin_amdgcn_ballot_w64(le);
+    const int A = mbcnt(bg, rge);
+    const int lin = mbcnt(bl, rle) + (le ? 1 : 0);
+    const bool cond = A + lin < tot_le;
+    const int sr = tot_le - lin + 1;
+    if (le && sr <= half) spos[sr] = (uint32_t)pos;
+    if (ge && cond) gpos[A + 1] = (uint32_t)pos;
+    const uint64_t bc = __builtin_amdgcn_ballot_w64(cond);
+    nsw += __popcll(bg & bc);
+    const uint64_t bf = bg & ~bc;
+    ff = min(ff, bf ? wbeg + j * 64 + (int)__builtin_ctzll(bf) : kBig);
+    rge += __popcll(bg);
+    rle += __popcll(bl);
+  }
+  if (lane == 0) {
+    sc.nsw[wid] = nsw;
+    sc.ff[wid] = ff;
+  }
+  __syncthreads();
+  int msw = 0, gnext = kBig;
+  for (int w = 0; w < kSelWaves; ++w) {
+    msw += sc.nsw[w];
+    gnext = min(gnext, sc.ff[w]);  // stripes ascend with the wave id
+  }
+  if (tid == 0) kv_swap(key, idx, lo, ch);  // the median move, made physical
+  __syncthreads();
+  // ---- P4: the m disjoint swaps g_t <-> s_t ----
+  for (int t = tid + 1; t <= msw; t += kSelThreads) {
+    const int g = (int)gpos[t], sv = (int)spos[t];
+    const KeyT kg = key[g], ks = key[sv];
+    const uint32_t ig = idx[g], is = idx[sv];
+    key[g] = ks;
+    key[sv] = kg;
+    idx[g] = is;
+    idx[sv] = ig;
+  }
+  const int cut = min(gnext, msw > 0 ? (int)spos[msw] : kBig);
+  __syncthreads();  // tables and counters are reused by the next level
+  return cut;
+}
+
+template <int DT>
+__global__ void __launch_bounds__(kSelThreads)
+    select_long_kernel(const LayerChunk T, int BH, int order, int algo,
+                       const char* __restrict__ norms, int64_t norm_stride,
+                       int32_t* __restrict__ out_idx, int64_t idx_stride,
+                       char* __restrict__ scratch, int64_t scratch_row_bytes, int n_cap) {
+  typedef typename DTypeTraits<DT>::key_t KeyT;
+  constexpr int ESZ = DTypeTraits<DT>::esz;
+  __shared__ SelScalars<KeyT> ssc;
+  __shared__ LongScalars sc;
+  const kvc_layer_t* ly = T.l + blockIdx.x / BH;
+  const int row = ly->row0 + (int)(blockIdx.x % BH);
+  const int n = ly->zone_len, k = ly->n_select;
+  if (k <= 0 || n <= 0 || n > n_cap || n > kZoneMaxLong) return;
+  const char* nrow = norms + (int64_t)row * norm_stride * ESZ;
+  int32_t* out = out_idx + (int64_t)row * idx_stride;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (k >= n) {
+    for (int i = tid; i < n; i += kSelThreads) out[i] = i;
+    return;
+  }
+  char* base = scratch + (int64_t)row * scratch_row_bytes;
+  KeyT* key = reinterpret_cast<KeyT*>(base);
+  uint32_t* idx = reinterpret_cast<uint32_t*>(base + (size_t)n_cap * sizeof(KeyT));
+  uint32_t* spos = idx + n_cap;
+  uint32_t* gpos = spos + (n_cap / 2 + 2);
+  const bool desc = order == KVC_DESC;
+  if (ly->score_mode == KVC_SCORE_SNAPKV) {  // unpooled scores in the idx region first
+    snapkv_keys<DT, KeyT, kSelThreads>(nrow, n, ly->pool_kernel, desc, key,
+                                       reinterpret_cast<char*>(idx), ssc);
+    __syncthreads();
+  } else {
+    for (int i = tid; i < n; i += kSelThreads) {
+      if constexpr (DT == KVC_F32)
+        key[i] = key_f32(f32_to_bits(load_dt<DT>(nrow, i)), desc);
+      else
+        key[i] = key16_dt<DT>(reinterpret_cast<const uint16_t*>(nrow)[i], desc);
+    }
+  }
+  for (int i = tid; i < n; i += kSelThreads) idx[i] = (uint32_t)i;
+  __syncthreads();
+  const bool topk = algo == KVC_ALGO_TOPK;
+  if (topk && (int64_t)k * 64 <= n) {  // std::partial_sort's heap select (one lane)
+    if (tid == 0) heap_select(key, idx, k, n);
+  } else {
+    const int thr = topk ? 3 : 16;
+    int lo = 0, hi = n, depth = 2 * floor_log2(n);
+    while (true) {
+      if (lo == k || hi == k) break;
+      if (hi - lo <= thr) {
+        if (tid == 0) insertion_sort(key, idx, lo, hi);
+        break;
+      }
+      if (depth == 0) {
+        if (tid == 0) {
+          if (topk) {
+            heap_select(key + lo, idx + lo, k - lo, hi - lo);
+            kv_swap(key, idx, lo, k - 1);
+          } else {
+            make_heap(key + lo, idx + lo, hi - lo);
+            sort_heap(key + lo, idx + lo, hi - lo);
+          }
+        }
+        break;
+      }
+      --depth;
+      const int cut = partition_long<KeyT>(key, idx, spos, gpos, sc, lo, hi);
+      if (topk) {
+        if (cut <= k - 1) lo = cut; else hi = cut;
+      } else {
+        if (k <= cut) hi = cut; else lo = cut;
+      }
+    }
+  }
+  __syncthreads();
+  // ---- emit {idx[0..k)} ascending: u16 flags over the (dead) key region, two counted passes
+  uint16_t* flag = reinterpret_cast<uint16_t*>(key);
+  for (int i = tid; i < n; i += kSelThreads) flag[i] = 0;
+  __syncthreads();
+  for (int i = tid; i < k; i += kSelThreads) flag[idx[i]] = 1;
+  __syncthreads();
+  const int J = (n + kSelThreads - 1) / kSelThreads;
+  const int wbeg = wid * J * 64;
+  int c = 0;
+  for (int j = 0; j < J; ++j) {
+    const int pos = wbeg + j * 64 + lane;
+    c += __popcll(__builtin_amdgcn_ballot_w64(pos < n && flag[pos] != 0));
+  }
+  if (lane == 0) sc.ge[wid] = c;
+  __syncthreads();
+  int run = 0;
+  for (int w = 0; w < wid; ++w) run += sc.ge[w];
+  for (int j = 0; j < J; ++j) {
+    const int pos = wbeg + j * 64 + lane;
+    const bool f = pos < n && flag[pos] != 0;
+    const uint64_t bf = __builtin_amdgcn_ballot_w64(f);
+    if (f) out[run + __popcll(bf & lanemask_lt(lane))] = pos;
+    run += __popcll(bf);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // GATHER
 // ---------------------------------------------------------------------------------------------
@@ -1267,6 +1477,7 @@ static inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; 
 static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 // one row of the global selection scratch (SelArrays for n_cap positions), 256-B aligned rows
 static inline size_t sel_scratch_row_bytes(int n_cap, int dtype) {
+  if (n_cap > kZoneMaxGlobal) return round_up(sel_long_bytes(n_cap, esize(dtype)), 256);
   return round_up(sel_bytes(n_cap, esize(dtype), n_cap / 2 + 1), 256);
 }
 
@@ -1298,7 +1509,7 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
     const int64_t n_out = (int64_t)y.sink_len + y.n_select + y.tail_len;
     if (n_out > 0x7FFFFFFF || 2 * BH * n_out * nc > 0x7FFFFFFF) return KVC_E_ARG;
     const bool needs_select = y.n_select > 0 && y.n_select < y.zone_len;
-    if (needs_select && y.zone_len > kZoneMaxGlobal) return KVC_E_TOO_LONG;
+    if (needs_select && y.zone_len > kZoneMaxLong) return KVC_E_TOO_LONG;
     if (n_out > 0) {
       if (!y.k || !y.v || !y.k_out || !y.v_out) return KVC_E_ARG;
       if (!aligned16(y.k) || !aligned16(y.v) || !aligned16(y.k_out) || !aligned16(y.v_out))
@@ -1437,7 +1648,7 @@ extern "C" {
 
 int kvc_version(void) { return KVC_ABI_VERSION; }
 size_t kvc_layer_struct_size(void) { return sizeof(kvc_layer_t); }
-int kvc_max_zone_len(void) { return kvc::kZoneMaxGlobal; }
+int kvc_max_zone_len(void) { return kvc::kZoneMaxLong; }
 
 const char* kvc_status_string(int s) {
   switch (s) {
@@ -1563,9 +1774,14 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
                                    (size_t)info.rows * info.index_row_stride * 4, 256);
       const int64_t rb = (int64_t)sel_scratch_row_bytes(n_cap, p->dtype);
       with_dtype(p->dtype, [&](auto dt) {
-        hipLaunchKernelGGL(select_global_kernel<decltype(dt)::value>, grid, block, 0, s, T, BH,
-                           p->order, p->algo, norms, info.norm_row_stride, idx,
-                           info.index_row_stride, wave_seg, scratch, rb, n_cap);
+        if (n_cap > kZoneMaxGlobal)  // u32 positions (the call's longest zone decides)
+          hipLaunchKernelGGL(select_long_kernel<decltype(dt)::value>, grid, block, 0, s, T, BH,
+                             p->order, p->algo, norms, info.norm_row_stride, idx,
+                             info.index_row_stride, scratch, rb, n_cap);
+        else
+          hipLaunchKernelGGL(select_global_kernel<decltype(dt)::value>, grid, block, 0, s, T, BH,
+                             p->order, p->algo, norms, info.norm_row_stride, idx,
+                             info.index_row_stride, wave_seg, scratch, rb, n_cap);
       });
     } else if ((p->phases & KVC_PHASE_SELECT) && sel && !p->external_index) {
       uint64_t* st = stamps ? stamps + (size_t)layers[c0].row0 * 32 : nullptr;

@@ -32,7 +32,7 @@ def test_struct_layout():
     assert ctypes.sizeof(N.Params) == 32
     assert ctypes.sizeof(N.PlanInfo) == 80
     assert L.kvc_version() == 1
-    assert L.kvc_max_zone_len() == 65536
+    assert L.kvc_max_zone_len() == 1 << 24
 
 
 def _layer(S, zs, zl, k, sink=0, ts=0, tl=0, ptr=4096):
@@ -102,7 +102,7 @@ def test_plan_rejects_bad_layers():
         (_layer(100, 0, 100, 101), -1),                # selecting more than the zone
         (_layer(100, 0, 100, 10, ts=95, tl=10), -1),   # tail past the end
         (_layer(100, 0, 100, 10, ptr=4100), -4),       # misaligned pointer
-        (_layer(70000, 0, 70000, 10), -5),             # zone longer than 65536 positions
+        (_layer((1 << 24) + 64, 0, (1 << 24) + 64, 10), -5),  # zone longer than 2^24 positions
     ]
     for t, code in cases:
         rc, _ = N.plan(_params(), np.array([t], dtype=N.LAYER_DTYPE))
@@ -126,6 +126,20 @@ def test_plan_long_zone_gets_global_scratch():
     idx_end = i1.index_offset + 32 * i1.index_row_stride * 4
     idx_end += -idx_end % 256
     assert i1.workspace_bytes == idx_end + 32 * row
+
+
+def test_plan_zone_beyond_u16_positions_gets_u32_scratch():
+    """Zones longer than 65536 positions select with u32 positions and full rank tables:
+    key | idx (u32) | two tables of n_cap/2 + 2 u32 ranks per row."""
+    t = np.array([_layer(100000, 0, 100000, 512)], dtype=N.LAYER_DTYPE)
+    rc, info = N.plan(_params(), t)
+    assert rc == 0
+    n_cap = 100000 + (-100000 % 64)
+    row = n_cap * 2 + n_cap * 4 + 2 * (n_cap // 2 + 2) * 4
+    row += -row % 256
+    idx_end = info.index_offset + 32 * info.index_row_stride * 4
+    idx_end += -idx_end % 256
+    assert info.workspace_bytes == idx_end + 32 * row
 
 
 def test_status_strings():

@@ -253,3 +253,33 @@ def test_zones_longer_than_lds_limit(dtype):
             rk, rv, _ = ref([(K, V)], **kw)[0]
             assert np.array_equal(to_np(out[0][0]), rk), (S, fn.__name__, kw)
             assert np.array_equal(to_np(out[0][1]), rv), (S, fn.__name__, kw)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16", "fp32"])
+def test_zones_beyond_u16_positions(dtype):
+    """Zones > 65536 positions: u32-position selection from a global scratch (select_long_kernel),
+    every path (introsort set asc/desc, introselect, partial-sort heap select, l2_compress's
+    large k) bit-exact against the oracle; a call mixing a long and a short layer."""
+    from kvcompress.methods import fix_size_l2_compress, l2_compress, snapkv_lite_compress
+    for S, variant in ((65600, "few"), (100000, "normal"), (131072, "equal")):
+        K = prng.gen_keys(8000 + S, (1, 2, S, 64), dtype, variant)
+        V = prng.gen_values(8000 + S, (1, 2, S, 64), dtype)
+        K2 = prng.gen_keys(9000 + S, (1, 2, 3000, 64), dtype, "few")
+        V2 = prng.gen_values(9000 + S, (1, 2, 3000, 64), dtype)
+        kv = [(to_dev(K), to_dev(V)), (to_dev(K2), to_dev(V2))]
+        for fn, ref, kw in (
+                (fix_size_l2_compress, oracle.fix_size_l2_compress,
+                 dict(fix_kv_size=700, keep_ratio=0.25, skip_layers=[])),
+                (fix_size_l2_compress, oracle.fix_size_l2_compress,
+                 dict(fix_kv_size=S // 3, strategy="keep_high", skip_layers=[])),
+                (snapkv_lite_compress, oracle.snapkv_lite_compress,
+                 dict(observation_window=32, keep_size=512, skip_layers=[])),
+                (snapkv_lite_compress, oracle.snapkv_lite_compress,
+                 dict(observation_window=32, keep_size=S // 2, skip_layers=[])),
+                (l2_compress, oracle.l2_compress,
+                 dict(keep_ratio=0.8, prune_after=100, skip_layers=[]))):
+            out = fn(list(kv), **kw)
+            refs = ref([(K, V), (K2, V2)], **kw)
+            for li, ((ko, vo), (rk, rv, _)) in enumerate(zip(out, refs)):
+                assert np.array_equal(to_np(ko), rk), (S, fn.__name__, kw, li)
+                assert np.array_equal(to_np(vo), rv), (S, fn.__name__, kw, li)
