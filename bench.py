@@ -138,20 +138,34 @@ def cpu_baseline(seq_len=S, head_dim=D, seconds=12.0, dtype="bf16"):
                       f"{threads} threads, {n1} layers in {dt1:.1f}s on 1 thread"}
 
 
-def ppl_delta(device, tokens=256, fix=64, keep_ratio=0.5):
-    """The metric's "PPL delta vs ref" half: teacher-forced evaluate_with_compression (one
-    compress call per token) of a random-init GPT-NeoX (pythia architecture, 4 layers, weights
-    unavailable offline) on `device`, once with the engine's fix_size_l2_compress and once with
-    the reference's CPU op sequence (oracle/torch_port.py, K/V copied to the host and back) as
-    compress_fn; same model, same synthetic token stream."""
+PPL_MODELS = {  # GPT-NeoX geometries (pythia configs; weights are random: none offline)
+    "pythia-2.8b": dict(vocab_size=50304, hidden_size=2560, num_hidden_layers=32,
+                        num_attention_heads=32, intermediate_size=10240),
+    "tiny": dict(vocab_size=512, hidden_size=256, num_hidden_layers=4, num_attention_heads=4,
+                 intermediate_size=1024),
+}
+
+
+def ppl_delta(device, arch="pythia-2.8b", tokens=2000, fix=512, keep_ratio=0.5):
+    """The metric's "PPL delta vs ref" half on BASELINE's config: teacher-forced
+    evaluate_with_compression (one compress call per token, skip_layers=[0, 1] as the
+    reference's default) of a random-init GPT-NeoX with pythia-2.8b's geometry (32 layers, 32
+    heads, D = 80; weights unavailable offline) in bf16 on `device`, once with the engine's
+    fix_size_l2_compress and once with the reference's CPU op sequence (oracle/torch_port.py,
+    K/V copied to the host and back) as compress_fn; same model, same synthetic token stream.
+    fix_kv_size=512 / keep_ratio=0.5 is the reference's README configuration; `tokens` > fix so
+    that ~tokens - fix steps compress (2000: the length of the reference's PG-19 samples)."""
     from transformers import GPTNeoXConfig, GPTNeoXForCausalLM
     from kvcompress.evaluate import evaluate_with_compression
     from kvcompress.methods import fix_size_l2_compress
     from oracle.torch_port import fix_size_l2_layer
 
-    class Tok:  # deterministic byte-level token stream
+    geo = PPL_MODELS[arch]
+
+    class Tok:  # deterministic synthetic token stream over the vocabulary
         def encode(self, text, return_tensors="pt"):
-            return torch.tensor([[(b * 7 + i) % 512 for i, b in enumerate(text.encode())]])
+            v = geo["vocab_size"]
+            return torch.tensor([[(b * 7919 + i * 104729) % v for i, b in enumerate(text.encode())]])
 
     def reference(kv, skip_layers=(), fix_kv_size=fix, keep_ratio=keep_ratio):
         out = []
@@ -164,21 +178,31 @@ def ppl_delta(device, tokens=256, fix=64, keep_ratio=0.5):
         return out
 
     torch.manual_seed(0)
-    cfg = GPTNeoXConfig(vocab_size=512, hidden_size=256, num_hidden_layers=4,
-                        num_attention_heads=4, intermediate_size=1024, rotary_pct=0.25,
-                        max_position_embeddings=4096)
-    model = GPTNeoXForCausalLM(cfg).to(torch.bfloat16).to(device).eval()
+    cfg = GPTNeoXConfig(rotary_pct=0.25, max_position_embeddings=2048, **geo)
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.bfloat16)
+    try:
+        with torch.device(device):
+            model = GPTNeoXForCausalLM(cfg).eval()
+    finally:
+        torch.set_default_dtype(prev)
     text = "The quick brown fox jumps over the lazy dog. " * (tokens // 40 + 1)
     kw = dict(fix_kv_size=fix, keep_ratio=keep_ratio)
+    t0 = time.perf_counter()
     r = [evaluate_with_compression(model, Tok(), text, compress_fn=fn, compress_kwargs=kw,
-                                   max_tokens=tokens, skip_layers=[0], show_progress=False)
+                                   max_tokens=tokens, skip_layers=[0, 1], show_progress=False)
          for fn in (fix_size_l2_compress, reference)]
+    dt = time.perf_counter() - t0
+    del model
+    torch.cuda.empty_cache()
     return {"value": r[0]["perplexity"] - r[1]["perplexity"], "ppl": r[0]["perplexity"],
             "ppl_ref": r[1]["perplexity"], "accuracy_delta": r[0]["accuracy"] - r[1]["accuracy"],
             "tokens": r[0]["num_tokens"], "final_cache_size": r[0]["final_cache_size"],
-            "sample": f"fix_size_l2(fix_kv_size={fix}, keep_ratio={keep_ratio}), skip_layers=[0], "
-                      "random-init 4-layer GPT-NeoX (pythia arch) bf16, synthetic tokens; "
-                      "engine vs the reference's CPU op sequence as compress_fn"}
+            "tpot_engine_s": r[0]["tpot"], "tpot_ref_cpu_compress_s": r[1]["tpot"],
+            "sample": f"fix_size_l2(fix_kv_size={fix}, keep_ratio={keep_ratio}), "
+                      f"skip_layers=[0, 1], random-init {arch} architecture (GPT-NeoX) bf16, "
+                      f"{r[0]['num_tokens']} synthetic tokens teacher-forced; engine vs the "
+                      f"reference's CPU op sequence as compress_fn ({dt:.0f} s)"}
 
 
 def timed_steps(step, steps, warmup, dist, sync, device, on_start=None):
@@ -245,6 +269,8 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=sorted(DTYPES),
                     help="K/V storage dtype (fp16: what transformers >= 5 loads pythia as)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ppl-model", default="pythia-2.8b", choices=sorted(PPL_MODELS),
+                    help="architecture of the random-init model of the PPL-delta leg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -343,9 +369,9 @@ def main():
         }
         ev = sum(kv[0].size(2) for kv in layers) - sum(kv[0].size(2) for kv in step())
         res["tokens_evicted_per_sec"] = ev * world * args.steps / elapsed
-        if not args.no_cpu_baseline and method == "fix_size_l2":
+        if not args.no_cpu_baseline and method == "fix_size_l2" and world == 1:  # N=1 only
             res["cpu_baseline"] = cpu_baseline(seq_len, head_dim, dtype=args.dtype)
-            res["ppl_delta_vs_ref"] = ppl_delta(dev)
+            res["ppl_delta_vs_ref"] = ppl_delta(dev, arch=args.ppl_model)
         print(json.dumps(res), flush=True)
     if dist:
         dist.barrier()
