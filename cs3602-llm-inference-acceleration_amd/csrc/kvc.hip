@@ -718,6 +718,117 @@ __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, uint16_t* gpo
   }
 }
 
+// Block-wide sum of one int per wave (waves of NT threads).  Callers alternate two buffers, so
+// consecutive calls need one barrier each (a wave can only rewrite a buffer after every wave has
+// passed the barrier of the call in between, i.e. finished reading it).
+template <int NT>
+__device__ __forceinline__ int block_sum_waves(int v, int* buf, int lane, int wid) {
+  static_assert(NT / 64 <= 16, "one 16-lane DPP row holds the wave sums");
+  if (lane == 0) buf[wid] = v;
+  __syncthreads();
+  const int s = row_scan16(lane < NT / 64 ? buf[lane] : 0);  // lanes 0..NW-1 = waves
+  return __builtin_amdgcn_readlane(s, NT / 64 - 1);
+}
+
+// No-straddling-tie fast path (32-bit keys): the k-th smallest key T by bisection over the key
+// values (the row's keys held in registers, one ballot count per step), with c_le = #keys <= T.
+// If c_le == k, every key <= T is kept and every other key is not, whatever order libstdc++'s
+// sort / nth_element / partial_sort would leave tied elements in -- the first-k SET is fixed by
+// the values alone.  fp32 norms essentially never tie at the boundary, so
+// this replaces the partition chain for them; bf16 / fp16 rows (tied in nearly every head) skip
+// it.  Returns true (and emits) when it applies.
+template <int NT, int JM, typename KeyT, bool TO_LDS>
+__device__ bool select_fast_untied(const KeyT* key, int n, int k, SelScalars<KeyT>& sc,
+                                   int32_t* out, uint16_t* sel) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = (NT == 64) ? 0 : uni(tid >> 6);
+  const int J = (n + NT - 1) / NT;
+  if (J > JM) return false;
+  const int wbeg = wid * J * 64;
+  // the row's keys in registers (every loop below is fully unrolled and predicated on j < J:
+  // a runtime trip count would turn kv[] into indexed register accesses)
+  uint32_t kv[JM];
+  uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+    const int pos = wbeg + j * 64 + lane;
+    const bool v = j < J && pos < n;
+    kv[j] = v ? (uint32_t)key[min(pos, n - 1)] : 0xFFFFFFFFu;
+    mn = v ? min(mn, kv[j]) : mn;
+    mx = v ? max(mx, kv[j]) : mx;
+  }
+  // block min / max of the keys: the bisection range
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+  }
+  if (lane == 0) {
+    sc.wa[wid] = (int)mn;
+    sc.wb[wid] = (int)mx;
+  }
+  __syncthreads();
+  uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    lo = min(lo, (uint32_t)sc.wa[w]);
+    hi = max(hi, (uint32_t)sc.wb[w]);
+  }
+  lo = (uint32_t)uni((int)lo);
+  hi = (uint32_t)uni((int)hi);
+  __syncthreads();  // sc.wa / sc.wb are the count buffers below
+  // smallest v with #(key <= v) >= k; invariant c_le = #(key <= hi) (= n at hi = max key)
+  int c_le = n, parity = 0;
+  while (lo < hi) {
+    const uint32_t mid = lo + ((hi - lo) >> 1);
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < JM; ++j) {
+      const int pos = wbeg + j * 64 + lane;
+      c += __popcll(__builtin_amdgcn_ballot_w64(j < J && pos < n && kv[j] <= mid));
+    }
+    const int tot = block_sum_waves<NT>(c, parity ? sc.wb : sc.wa, lane, wid);
+    parity ^= 1;
+    if (tot >= k) {
+      hi = mid;
+      c_le = tot;
+    } else {
+      lo = mid + 1;
+    }
+  }
+  if (c_le != k) {
+    __syncthreads();  // the chain reuses sc
+    return false;
+  }
+  // ---- emit {pos : key[pos] <= T} ascending ----
+  const uint32_t T = lo;
+  uint32_t fm = 0;  // kept flags by j
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+    const int pos = wbeg + j * 64 + lane;
+    const bool f = j < J && pos < n && kv[j] <= T;
+    fm |= f ? (1u << j) : 0u;
+    c += __popcll(__builtin_amdgcn_ballot_w64(f));
+  }
+  if (lane == 0) sc.wm[wid] = c;
+  __syncthreads();
+  int run = 0;
+  for (int w = 0; w < wid; ++w) run += sc.wm[w];
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+    const int pos = wbeg + j * 64 + lane;
+    const bool f = (fm >> j) & 1u;
+    const uint64_t bf = __builtin_amdgcn_ballot_w64(f);
+    if (f) {
+      const int r = run + __popcll(bf & lanemask_lt(lane));
+      if constexpr (TO_LDS) sel[r] = (uint16_t)pos;
+      else out[r] = pos;
+    }
+    run += __popcll(bf);
+  }
+  return true;
+}
+
 // Reference-exact selection for one (layer, b, h) row whose zone norms are at `nrow`; working
 // arrays at `arrays` (SelArrays layout for n_cap positions and `cap`-rank windows: LDS, or a
 // global scratch row for zones longer than kZoneMax) and scalars in `sc`; NT threads (the
@@ -802,6 +913,13 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
   KVC_STAMP(1);
 
   // ---- reference-exact k-selection ----
+  if constexpr (sizeof(KeyT) == 4 && MAXJ <= 16) {  // fp32 keys: untied boundary -> values only
+    // (`sel` may alias the key region: the keys are read into registers before any store)
+    if (select_fast_untied<NT, MAXJ, KeyT, TO_LDS>(key, n, k, sc, out, sel)) {
+      KVC_STAMP(31);  // diagnostic build: fast path taken
+      return;
+    }
+  }
   const bool topk = algo == KVC_ALGO_TOPK;
   const bool partial = topk && (int64_t)k * 64 <= n;  // aten TopKImpl.h: use_partial_sort
   const int thr = topk ? 3 : 16;  // introselect / introsort segment threshold

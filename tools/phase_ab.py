@@ -1,0 +1,33 @@
+"""Per-phase kernel times of one library build (select KVC_LIB to A/B builds in separate
+processes; GPU box, tuning aid).  32 layers of [1,32,S,128] in AB_DTYPE, fix_size_l2(512):
+SCORE / SELECT / GATHER as three timed launches, and SCORE / SELECT_GATHER as the default two."""
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cs3602-llm-inference-acceleration_amd"))
+from kvcompress import _engine  # noqa: E402
+from kvcompress.methods import fix_size_l2_compress  # noqa: E402
+
+dev = torch.device("cuda:0")
+dt = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[
+    os.environ.get("AB_DTYPE", "fp32")]
+S = int(os.environ.get("AB_S", "16384"))
+g = torch.Generator(device=dev).manual_seed(0)
+layers = [(torch.randn(1, 32, S, 128, device=dev, generator=g).to(dt),
+           torch.randn(1, 32, S, 128, device=dev, generator=g).to(dt)) for _ in range(32)]
+res = {"lib": os.path.basename(os.environ.get("KVC_LIB", "libkvc.so")), "dtype": str(dt)}
+for name, steps in (("three", _engine.PhaseTimer.THREE), ("two", _engine.PhaseTimer.DEFAULT)):
+    os.environ["KVC_SEL_GATHER"] = "0" if name == "three" else "1"
+    for _ in range(3):
+        fix_size_l2_compress(layers, fix_kv_size=512, skip_layers=[])
+    t = _engine.PhaseTimer(steps=steps)
+    _engine.set_phase_timer(t)
+    for _ in range(10):
+        fix_size_l2_compress(layers, fix_kv_size=512, skip_layers=[])
+    _engine.set_phase_timer(None)
+    res[name] = {k: round(sum(v) / len(v), 4) for k, v in t.durations_ms().items()}
+print(json.dumps(res))
