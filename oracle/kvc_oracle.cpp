@@ -131,6 +131,28 @@ extern "C" {
 
 int orc_version(void) { return 1; }
 
+// tests/golden/prng.py normal_f32 restated (same integer and IEEE double operations, no
+// contraction), for speed only: the fixtures' input hashes check that both agree.
+//   z = seed + i * golden (i = offset + 1 ...), splitmix64 finaliser, u = (z >> 11) * 2^-53,
+//   x = ((((u0 + u1) + u2) + u3) - 2) * sqrt(3) per output, RNE to fp32.
+int orc_normal_f32(uint64_t seed, int64_t n, float* out) {
+  const uint64_t golden = 0x9E3779B97F4A7C15ull, m1 = 0xBF58476D1CE4E5B9ull,
+                 m2 = 0x94D049BB133111EBull;
+  const double sqrt3 = 1.7320508075688772;
+  for (int64_t j = 0; j < n; ++j) {
+    double u[4];
+    for (int q = 0; q < 4; ++q) {
+      uint64_t z = seed + (uint64_t)(4 * j + q + 1) * golden;
+      z = (z ^ (z >> 30)) * m1;
+      z = (z ^ (z >> 27)) * m2;
+      z = z ^ (z >> 31);
+      u[q] = (double)(z >> 11) * (1.0 / 9007199254740992.0);
+    }
+    out[j] = (float)(((((u[0] + u[1]) + u[2]) + u[3]) - 2.0) * sqrt3);
+  }
+  return 0;
+}
+
 // Storage rounding of fp32 values (bit patterns out), for the conversion tests.
 int orc_to_dtype_bits(int dtype, const float* in, int64_t n, uint32_t* out) {
   for (int64_t i = 0; i < n; ++i)

@@ -84,3 +84,12 @@ def test_oracle_snapkv_scores_match_torch_golden(idx):
     np.testing.assert_array_equal(bits(oracle.snapkv_scores(n, 1)), bits(arrs[p["key"] + "_scores"]))
     np.testing.assert_array_equal(bits(oracle.snapkv_scores(n, p["pool"])),
                                   bits(arrs[p["key"] + "_pooled"]))
+
+
+def test_prng_c_restatement_matches_numpy():
+    """prng.normal_f32 uses oracle/liboracle.so's restatement when built; it must reproduce the
+    numpy generator the fixtures were made with bit for bit (incl. across its 2^22 chunks)."""
+    assert prng._clib(), "liboracle.so (make -C oracle) not built"
+    for seed, n in ((1, 1000), (0xABCDEF ^ 1234, 123457), (2 ** 63 + 5, (4 << 20) + 17)):
+        a, b = prng.normal_f32(seed, n), prng.normal_f32_numpy(seed, n)
+        np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
