@@ -349,7 +349,7 @@ def main():
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (torch.randn, HBM-resident)",
-            "config": {"workload": f"{method}_compress({cfg_kw}, skip_layers=[]) over "
+            "config": {"workload": f"{method if method.endswith('_compress') else method + '_compress'}({cfg_kw}, skip_layers=[]) over "
                                    f"{n_layers} layers of K,V [1,{H},{seq_len},{head_dim}] per "
                                    f"GPU, one call per step ({what})",
                        "name": args.workload, "layers_per_gpu": n_layers,
