@@ -3,43 +3,17 @@ kvcompress package (reference: kvcompress/__init__.py:1-97).
 
 The compress functions keep the reference's signatures, registry and results (bit-exact
 indices, byte-identical K/V); their norm / top-k / gather work runs in hand-written HIP kernels
-for gfx950 (libkvc.so, C ABI in include/kvc.h).
+for gfx950 (libkvc.so, C ABI in include/kvc.h).  Top-level names: the reference's exports.
 """
-from .methods import (
-    l2_compress,
-    fix_size_l2_compress,
-    streaming_llm_compress,
-    get_compress_fn,
-    list_methods,
-    register_method,
-    COMPRESS_METHODS,
-)
-from .evaluate import (
-    evaluate_with_compression,
-    evaluate_baseline,
-    compare_methods,
-)
-from .benchmark import (
-    benchmark,
-    measure_generation_metrics,
-    run_benchmark_suite,
-    print_benchmark_summary,
-)
-from .utils import (
-    to_dynamic_cache,
-    normalize_kv_cache,
-    get_cache_size_mb,
-    get_cache_info,
-    get_seq_len,
-)
+from .benchmark import (benchmark, measure_generation_metrics, print_benchmark_summary,
+                        run_benchmark_suite)
+from .evaluate import compare_methods, evaluate_baseline, evaluate_with_compression
+from .methods import (COMPRESS_METHODS, fix_size_l2_compress, get_compress_fn, l2_compress,
+                      list_methods, register_method, streaming_llm_compress)
+from .utils import (get_cache_info, get_cache_size_mb, get_seq_len, normalize_kv_cache,
+                    to_dynamic_cache)
 
-__all__ = [
-    "l2_compress", "fix_size_l2_compress", "streaming_llm_compress",
-    "get_compress_fn", "list_methods", "register_method", "COMPRESS_METHODS",
-    "evaluate_with_compression", "evaluate_baseline", "compare_methods",
-    "benchmark", "measure_generation_metrics", "run_benchmark_suite", "print_benchmark_summary",
-    "to_dynamic_cache", "normalize_kv_cache", "get_cache_size_mb", "get_cache_info",
-    "get_seq_len",
-]
+__version__ = "2.0.0"  # the reference package version this mirrors
 
-__version__ = "2.0.0"
+__all__ = sorted(name for name in dir() if not name.startswith("_") and name not in (
+    "benchmark_module", "methods", "evaluate", "utils"))

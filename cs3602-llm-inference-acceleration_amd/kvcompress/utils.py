@@ -1,68 +1,64 @@
-"""KV cache format helpers -- same API as the reference's kvcompress/utils.py:12-116.
+"""Cache-format helpers with the API of the reference's kvcompress/utils.py:12-116.
 
-normalize_kv_cache additionally accepts transformers-5 caches (whose iteration the reference
-cannot unpack); for lists and legacy caches it behaves identically.
+`normalize_kv_cache` also unpacks transformers >= 5 caches, whose iteration yields 3-tuples the
+reference cannot unpack; for tuple lists and legacy caches it returns what
+the reference returns.
 """
-from typing import List, Tuple, Union
+from typing import List, Tuple
 
 import torch
 
+KVList = List[Tuple[torch.Tensor, torch.Tensor]]
 
-def _dynamic_cache_cls():
+
+def to_dynamic_cache(past_key_values: KVList):
+    """A transformers DynamicCache filled layer by layer with update(k, v, i) (utils.py:12-27)."""
     from transformers import DynamicCache
-    return DynamicCache
-
-
-def to_dynamic_cache(past_key_values: List[Tuple[torch.Tensor, torch.Tensor]]):
-    """utils.py:12-27: DynamicCache rebuilt with update(k, v, layer_idx) per layer."""
-    cache = _dynamic_cache_cls()()
-    for layer_idx, (keys, values) in enumerate(past_key_values):
-        cache.update(keys, values, layer_idx)
+    cache = DynamicCache()
+    for i, kv in enumerate(past_key_values):
+        cache.update(kv[0], kv[1], i)
     return cache
 
 
-def normalize_kv_cache(past_key_values) -> List[Tuple[torch.Tensor, torch.Tensor]]:
-    """utils.py:30-44: legacy tuple list out of any supported cache object."""
-    if hasattr(past_key_values, "to_legacy_cache"):
-        return past_key_values.to_legacy_cache()
+def normalize_kv_cache(past_key_values) -> KVList:
+    """(K, V) list view of a cache object (utils.py:30-44): legacy caches through
+    to_legacy_cache(), transformers-5 caches through their per-layer keys / values."""
+    legacy = getattr(past_key_values, "to_legacy_cache", None)
+    if legacy is not None:
+        return legacy()
     layers = getattr(past_key_values, "layers", None)
     if layers is not None and all(hasattr(l, "keys") and hasattr(l, "values") for l in layers):
-        return [(l.keys, l.values) for l in layers]  # transformers >= 5 DynamicCache
+        return [(l.keys, l.values) for l in layers]
     return list(past_key_values)
 
 
+def _nbytes(t: torch.Tensor) -> int:
+    return t.element_size() * t.nelement()
+
+
 def get_cache_size_mb(past_key_values) -> float:
-    """utils.py:47-65"""
-    past_key_values = normalize_kv_cache(past_key_values)
-    total = 0
-    for keys, values in past_key_values:
-        total += keys.element_size() * keys.nelement()
-        total += values.element_size() * values.nelement()
-    return total / (1024 ** 2)
+    """K and V bytes of every layer, in MiB (utils.py:47-65)."""
+    return sum(_nbytes(k) + _nbytes(v) for k, v in normalize_kv_cache(past_key_values)) / 2 ** 20
 
 
 def get_cache_info(past_key_values) -> dict:
-    """utils.py:68-94"""
-    past_key_values = normalize_kv_cache(past_key_values)
-    if not past_key_values:
+    """Layer count, per-layer sequence lengths and their min / max / mean, total MiB
+    (utils.py:68-94; an empty cache reports zeros)."""
+    layers = normalize_kv_cache(past_key_values)
+    if not layers:
         return {"num_layers": 0, "seq_lengths": [], "total_size_mb": 0}
-    seq_lengths = [keys.size(2) for keys, values in past_key_values]
-    return {
-        "num_layers": len(past_key_values),
-        "seq_lengths": seq_lengths,
-        "min_seq_len": min(seq_lengths),
-        "max_seq_len": max(seq_lengths),
-        "avg_seq_len": sum(seq_lengths) / len(seq_lengths),
-        "total_size_mb": get_cache_size_mb(past_key_values),
-    }
+    lens = [k.size(2) for k, _ in layers]
+    return {"num_layers": len(layers), "seq_lengths": lens, "min_seq_len": min(lens),
+            "max_seq_len": max(lens), "avg_seq_len": sum(lens) / len(lens),
+            "total_size_mb": get_cache_size_mb(layers)}
 
 
 def get_seq_len(past_key_values, layer_idx: int = 0) -> int:
-    """utils.py:97-116"""
-    past_key_values = normalize_kv_cache(past_key_values)
-    if not past_key_values or layer_idx >= len(past_key_values):
+    """Sequence length of one layer, 0 when the cache has no such layer (utils.py:97-116)."""
+    layers = normalize_kv_cache(past_key_values)
+    if len(layers) == 0 or layer_idx >= len(layers):
         return 0
-    return past_key_values[layer_idx][0].size(2)
+    return layers[layer_idx][0].size(2)  # negative indices count from the end, as there
 
 
 __all__ = ["to_dynamic_cache", "normalize_kv_cache", "get_cache_size_mb", "get_cache_info",

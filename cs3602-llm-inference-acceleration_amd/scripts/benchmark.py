@@ -268,67 +268,57 @@ def build_methods_config(args) -> list:
     return methods
 
 
+# (flag, type, default, help) -- the reference's argument surface (scripts/benchmark.py:551-626):
+# same flags, types, defaults and choices; store_true flags have type None
+_METHOD_CHOICES = ["l2_compress", "fix_size_l2", "streaming_llm", "h2o_l2", "snapkv_lite",
+                   "pyramid_kv", "adaptive_l2"]
+_ARGS = (
+    ("--model_id", str, "EleutherAI/pythia-2.8b", "HF model id (cache first, then the Hub)"),
+    ("--num_samples", int, 2, "PG-19 samples"),
+    ("--max_tokens", int, 2000, "tokens of the teacher-forced PPL pass"),
+    ("--max_new_tokens", int, 500, "generated tokens (TTFT / TPOT)"),
+    ("--skip_layers", str, "0,1", "layers never compressed, comma-separated"),
+    ("--no_baseline", None, False, "do not run the uncompressed baseline"),
+    ("--no_recent_only", None, False, "no recent_only control group for fixed-size methods"),
+    ("--num_warmup", int, 3, "warmup iterations"),
+    ("--method", str, None, "method to sweep"),
+    ("--compare_all", None, False, "every method at the 512 / 1024 defaults"),
+    ("--compare_new", None, False, "the newer methods (selects none, as in the reference)"),
+    ("--keep_ratios", str, "0.8,0.5,0.3", "keep_ratio list (l2_compress, fix_size_l2)"),
+    ("--prune_after", int, 100, "l2_compress: compress only beyond this length"),
+    ("--fix_kv_sizes", str, "256,512", "fix_size_l2: cache sizes"),
+    ("--strategies", str, "keep_low", "fix_size_l2: keep_low / keep_high / random"),
+    ("--start_size", int, 4, "attention-sink tokens"),
+    ("--recent_sizes", str, "252,508,1020", "streaming_llm: recent windows"),
+    ("--heavy_hitter_sizes", str, "32,64,128", "h2o_l2: heavy hitters"),
+    ("--h2o_recent_size", int, 444, "h2o_l2: recent window"),
+    ("--observation_windows", str, "16,32,64", "snapkv_lite: observation windows"),
+    ("--snapkv_keep_sizes", str, "512", "snapkv_lite: kept tokens"),
+    ("--base_sizes", str, "256,512", "pyramid_kv: first-layer budgets"),
+    ("--layer_decay", float, 0.9, "pyramid_kv: per-layer decay"),
+    ("--min_size", int, 64, "pyramid_kv: smallest per-layer budget"),
+    ("--pyramid_profile", str, "exponential", "pyramid_kv: budget profile"),
+    ("--target_sizes", str, "256,512", "adaptive_l2: target sizes"),
+    ("--soft_limit", int, 256, "adaptive_l2: no compression up to this length"),
+    ("--hard_limit", int, 1024, "adaptive_l2: full compression beyond this length"),
+    # offline extensions (not in the reference)
+    ("--random_model", str, None, "[offline] random-weight GPT-NeoX of this geometry"),
+    ("--text_file", str, None, "[offline] samples from a local text file"),
+    ("--synthetic_text", None, False, "[offline] deterministic pseudo-text samples"),
+)
+_CHOICES = {"--method": _METHOD_CHOICES, "--pyramid_profile": ["exponential", "linear", "constant"],
+            "--random_model": sorted(RANDOM_MODELS)}
+
+
 def build_parser():
     p = argparse.ArgumentParser(description="Unified Benchmark for KV Cache Compression",
                                 formatter_class=argparse.RawDescriptionHelpFormatter)
-    a = p.add_argument
-    a("--model_id", type=str, default="EleutherAI/pythia-2.8b", help="Model ID from HuggingFace")
-    a("--num_samples", type=int, default=2, help="Number of PG-19 samples to test")
-    a("--max_tokens", type=int, default=2000, help="Maximum tokens for PPL evaluation")
-    a("--max_new_tokens", type=int, default=500,
-      help="Number of tokens to generate for TTFT/TPOT")
-    a("--skip_layers", type=str, default="0,1", help="Comma-separated layer indices to skip")
-    a("--no_baseline", action="store_true", help="Skip baseline (no compression) benchmark")
-    a("--no_recent_only", action="store_true",
-      help="Skip recent_only (sliding window) control group for fixed-size methods")
-    a("--num_warmup", type=int, default=3,
-      help="Number of warmup iterations before benchmark (default: 3)")
-    a("--method", type=str, choices=["l2_compress", "fix_size_l2", "streaming_llm", "h2o_l2",
-                                     "snapkv_lite", "pyramid_kv", "adaptive_l2"],
-      help="Compression method to benchmark")
-    a("--compare_all", action="store_true",
-      help="Compare all original methods with default configurations")
-    a("--compare_new", action="store_true",
-      help="Compare new methods (H2O-L2, SnapKV-Lite, Pyramid, Adaptive)")
-    a("--keep_ratios", type=str, default="0.8,0.5,0.3",
-      help="Comma-separated keep_ratio values (for l2_compress)")
-    a("--prune_after", type=int, default=100,
-      help="Only compress after this many tokens (for l2_compress)")
-    a("--fix_kv_sizes", type=str, default="256,512",
-      help="Comma-separated fix_kv_size values (for fix_size_l2)")
-    a("--strategies", type=str, default="keep_low",
-      help="Comma-separated strategies: keep_low,keep_high,random")
-    a("--start_size", type=int, default=4, help="Number of initial tokens (attention sinks)")
-    a("--recent_sizes", type=str, default="252,508,1020",
-      help="Comma-separated recent_size values for StreamingLLM")
-    a("--heavy_hitter_sizes", type=str, default="32,64,128",
-      help="Comma-separated heavy_hitter_size values for H2O-L2")
-    a("--h2o_recent_size", type=int, default=444,
-      help="Recent window size for H2O-L2 (default: 444)")
-    a("--observation_windows", type=str, default="16,32,64",
-      help="Comma-separated observation_window values for SnapKV-Lite")
-    a("--snapkv_keep_sizes", type=str, default="512",
-      help="Comma-separated keep_size values for SnapKV-Lite")
-    a("--base_sizes", type=str, default="256,512",
-      help="Comma-separated base_size values for Pyramid KV")
-    a("--layer_decay", type=float, default=0.9,
-      help="Layer decay factor for Pyramid KV (default: 0.9)")
-    a("--min_size", type=int, default=64,
-      help="Minimum cache size for any layer in Pyramid KV (default: 64)")
-    a("--pyramid_profile", type=str, default="exponential",
-      choices=["exponential", "linear", "constant"],
-      help="Pyramid profile: exponential, linear, or constant")
-    a("--target_sizes", type=str, default="256,512",
-      help="Comma-separated target_size values for Adaptive L2")
-    a("--soft_limit", type=int, default=256,
-      help="Soft limit (no compression below this) for Adaptive L2")
-    a("--hard_limit", type=int, default=1024,
-      help="Hard limit (max compression above this) for Adaptive L2")
-    # offline extensions
-    a("--random_model", type=str, default=None, choices=sorted(RANDOM_MODELS),
-      help="[offline] random-weight GPT-NeoX of this geometry instead of --model_id")
-    a("--text_file", type=str, default=None, help="[offline] samples from a local text file")
-    a("--synthetic_text", action="store_true", help="[offline] deterministic pseudo-text samples")
+    for flag, typ, default, help_text in _ARGS:
+        if typ is None:
+            p.add_argument(flag, action="store_true", help=help_text)
+        else:
+            p.add_argument(flag, type=typ, default=default, choices=_CHOICES.get(flag),
+                           help=help_text)
     return p
 
 
