@@ -1,7 +1,7 @@
 """Randomised GPU parity: seeded random method / kwargs / geometry / dtype / key distribution,
 engine vs the CPU oracle, bit-exact K/V and identical output kinds.  Each case mixes several
-layers (ragged lengths, skip lists) in one call, so batching, per-layer branches and the
-launch-path variants are exercised together.  Seeds are fixed: a failure names its case."""
+layers (ragged lengths, skip lists) in one call, so batching and per-layer branches are
+exercised together; the three launch paths take turns.  Seeds are fixed: a failure names its case."""
 import numpy as np
 import pytest
 
@@ -39,8 +39,11 @@ def _kwargs(rng, method, S):
 
 
 @pytest.mark.parametrize("case", range(N_CASES))
-def test_random_configs_match_oracle(case):
+def test_random_configs_match_oracle(case, monkeypatch):
     from kvcompress.methods import get_compress_fn
+    # launch paths in rotation: SCORE + SELECT_GATHER, three kernels, the fused persistent kernel
+    monkeypatch.setenv("KVC_SEL_GATHER", "0" if case % 3 == 1 else "1")
+    monkeypatch.setenv("KVC_FUSED", "1" if case % 3 == 2 else "0")
     rng = np.random.default_rng(90000 + case)
     method = str(rng.choice(["fix_size_l2", "l2_compress", "streaming_llm", "h2o_l2",
                              "snapkv_lite", "pyramid_kv", "adaptive_l2", "recent_only"]))
