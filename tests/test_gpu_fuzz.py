@@ -2,6 +2,8 @@
 engine vs the CPU oracle, bit-exact K/V and identical output kinds.  Each case mixes several
 layers (ragged lengths, skip lists) in one call, so batching and per-layer branches are
 exercised together; the three launch paths take turns.  Seeds are fixed: a failure names its case."""
+import os
+
 import numpy as np
 import pytest
 
@@ -11,7 +13,7 @@ from oracle import oracle
 
 pytestmark = pytest.mark.gpu
 
-N_CASES = 300
+N_CASES = int(os.environ.get("KVC_FUZZ_CASES", "300"))  # more for a soak run
 
 
 def _kwargs(rng, method, S):
