@@ -780,12 +780,12 @@ __device__ bool select_fast_untied(const KeyT* key, int n, int k, SelScalars<Key
   int c_le = n, parity = 0;
   while (lo < hi) {
     const uint32_t mid = lo + ((hi - lo) >> 1);
-    int c = 0;
+    int cl = 0;  // per-lane count (VALU), one wave reduction per step
 #pragma unroll
-    for (int j = 0; j < JM; ++j) {
-      const int pos = wbeg + j * 64 + lane;
-      c += __popcll(__builtin_amdgcn_ballot_w64(j < J && pos < n && kv[j] <= mid));
-    }
+    for (int j = 0; j < JM; ++j) cl += (kv[j] <= mid) ? 1 : 0;  // invalid slots hold ~0u
+    const int rs = row_scan16(cl);
+    const int c = __builtin_amdgcn_readlane(rs, 15) + __builtin_amdgcn_readlane(rs, 31) +
+                  __builtin_amdgcn_readlane(rs, 47) + __builtin_amdgcn_readlane(rs, 63);
     const int tot = block_sum_waves<NT>(c, parity ? sc.wb : sc.wa, lane, wid);
     parity ^= 1;
     if (tot >= k) {
