@@ -454,6 +454,15 @@ __device__ __forceinline__ int row_scan16(int v) {
   v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);  // row_shr:8
   return v;
 }
+// popcount of a wave-uniform mask on the VALU (v_bcnt reading the SGPRs; the result in every
+// lane): a scalar s_bcnt1 of a mask a VALU compare has just written waits for that compare
+__device__ __forceinline__ int vpopc(uint64_t m) {
+  int r;
+  asm("v_bcnt_u32_b32 %0, %1, 0\n\tv_bcnt_u32_b32 %0, %2, %0"
+      : "=&v"(r)
+      : "s"((uint32_t)m), "s"((uint32_t)(m >> 32)));
+  return r;
+}
 // lanes below this one with their bit set in `mask`, plus `base` (v_mbcnt_lo/hi: 2 VALU)
 __device__ __forceinline__ int mbcnt(uint64_t mask, int base) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
@@ -957,26 +966,34 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
   const int J = (n + NT - 1) / NT;
   const int wbeg = wid * J * 64;
   uint64_t fm = 0;  // J <= 64
-  int c = 0;
+  int cl = 0;       // per-lane count: no scalar popcount waits on a ballot inside the loop
   for (int j = 0; j < J; ++j) {
     const int pos = wbeg + j * 64 + lane;
     const bool f = pos < n && flag[pos] != 0;
     fm |= (uint64_t)f << j;
-    c += __popcll(__ballot(f));
+    cl += f ? 1 : 0;
   }
-  if (lane == 0) sc.wa[wid] = c;
+  {
+    const int rs = row_scan16(cl);
+    const int c = __builtin_amdgcn_readlane(rs, 15) + __builtin_amdgcn_readlane(rs, 31) +
+                  __builtin_amdgcn_readlane(rs, 47) + __builtin_amdgcn_readlane(rs, 63);
+    if (lane == 0) sc.wa[wid] = c;
+  }
   __syncthreads();
-  int run = 0;
-  for (int w = 0; w < wid; ++w) run += sc.wa[w];
+  int run = 0;  // kept positions in the waves before this one
+  if constexpr (NT > 64) {
+    const int ws = row_scan16(lane < NT / 64 ? sc.wa[lane] : 0);
+    run = wid ? __builtin_amdgcn_readlane(ws, wid - 1) : 0;
+  }
   for (int j = 0; j < J; ++j) {
     const bool f = (fm >> j) & 1;
     const uint64_t bf = __ballot(f);
     if (f) {
-      const int r = run + __popcll(bf & lanemask_lt(lane));
+      const int r = mbcnt(bf, run);
       if constexpr (TO_LDS) sel[r] = (uint16_t)(wbeg + j * 64 + lane);
       else out[r] = wbeg + j * 64 + lane;
     }
-    run += __popcll(bf);
+    run += vpopc(bf);
   }
   KVC_STAMP(4);
 }
