@@ -3,18 +3,24 @@ keep_ratio=0.0, keep_low) on synthetic [1,32,16384,128] bf16 KV, 32 layers per G
 
 One step = one drop-in `fix_size_l2_compress(kv_list, ...)` call over all 32 layers (norm scoring
 of 16384 positions x 32 heads per layer, reference-exact selection, gather of 512 K/V rows).
-Inputs are resident in HBM before the timed region.  Multi-GPU: one process per GPU (torchrun),
-each rank owns 32 layers of a 32*N-layer stack (layers sharded, no collectives on the data
-path; weak scaling); a barrier + synchronize brackets the timed region and the max over ranks
-is reported.  Prints ONE JSON line on rank 0.
+Inputs are resident in HBM before the timed region.  Multi-GPU: one process per GPU, each rank
+owns 32 layers of a 32*N-layer stack (layers sharded, no collectives on the data path; weak
+scaling); a barrier + synchronize brackets the timed region and the max over ranks is reported.
+Prints ONE JSON line on rank 0.  Ranks come from torchrun (RANK / LOCAL_RANK / WORLD_SIZE in the
+environment) or, for `--gpus N` without them, from N child processes this script starts before
+anything touches the GPU (the parent only waits for them).
 
 `--workload` selects one of the other BASELINE / SURVEY §8(d) configurations (same contract, same
 JSON line; the default is the headline).  `--layers-total L` shards an L-layer model over the
-ranks instead (strong scaling, global layer indices; e.g. cfg4: h2o_l2, 32 layers over 8 GPUs).
+ranks instead (strong scaling, global layer indices; e.g. cfg4: h2o_l2, 32 layers over 8 GPUs);
+the `cfg4-*` / `cfg5-*` workloads default to that 32-layer split.  `--dry-run` runs the launch,
+timing and reporting harness on CPU with gloo and a stand-in step (tests/test_bench_launch.py).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -49,7 +55,16 @@ WORKLOADS = {
     "l2-s16384": ("l2_compress", dict(keep_ratio=0.8, prune_after=100), 16384, 80,
                   "cfg1 method (one-shot), pythia-2.8b"),
     "adaptive-s16384": ("adaptive_l2", dict(), 16384, 128, "adaptive_l2 defaults"),
+    # BASELINE configs[3] / [4] as named: ONE 32-layer model sharded over the ranks (strong
+    # scaling; 4 layers per GPU at N=8), global layer ids (skip_layers, pyramid depth)
+    "cfg4-h2o-l32": ("h2o_l2", dict(start_size=4, heavy_hitter_size=64, recent_size=444), 16384,
+                     80, "cfg4, pythia-2.8b, 32 layers sharded over the GPUs"),
+    "cfg5-snapkv-l32": ("snapkv_lite", dict(observation_window=32, keep_size=512), 16384, 128,
+                        "cfg5, pythia-6.9b, 32 layers sharded over the GPUs"),
+    "cfg5-pyramid-l32": ("pyramid_kv", dict(base_size=512), 16384, 128,
+                         "cfg5, pythia-6.9b, 32 layers sharded over the GPUs"),
 }
+STRONG_DEFAULT = {"cfg4-h2o-l32": 32, "cfg5-snapkv-l32": 32, "cfg5-pyramid-l32": 32}
 HEADLINE = "fix512-s16384"
 
 
@@ -120,6 +135,8 @@ def cpu_baseline(seq_len=S, head_dim=D, seconds=12.0, dtype="bf16"):
             n += 1
         return n, time.perf_counter() - t0
 
+    print(f"[bench] cpu_baseline: {seconds:.0f} s on {threads} threads + 1 thread",
+          file=sys.stderr, flush=True)
     n, dt = rate(seconds)
     torch.set_num_threads(1)  # also a 1-thread run
     n1, dt1 = rate(seconds / 3)
@@ -151,8 +168,10 @@ def ppl_delta(device, arch="pythia-2.8b", tokens=2000, fix=512, keep_ratio=0.5):
     evaluate_with_compression (one compress call per token, skip_layers=[0, 1] as the
     reference's default) of a random-init GPT-NeoX with pythia-2.8b's geometry (32 layers, 32
     heads, D = 80; weights unavailable offline) in bf16 on `device`, once with the engine's
-    fix_size_l2_compress and once with the reference's CPU op sequence (oracle/torch_port.py,
-    K/V copied to the host and back) as compress_fn; same model, same synthetic token stream.
+    fix_size_l2_compress and once with the reference's CPU op sequence (oracle/torch_port.py: norm -> argsort -> sort ->
+    gather -> cat, every branch of fix_size_l2.py:76-150, pinned to the unmodified reference's
+    golden outputs by tests/test_torch_port.py; K/V copied to the host and back) as compress_fn;
+    same model, same synthetic token stream.
     fix_kv_size=512 / keep_ratio=0.5 is the reference's README configuration; `tokens` > fix so
     that ~tokens - fix steps compress (2000: the length of the reference's PG-19 samples)."""
     from transformers import GPTNeoXConfig, GPTNeoXForCausalLM
@@ -169,7 +188,7 @@ def ppl_delta(device, arch="pythia-2.8b", tokens=2000, fix=512, keep_ratio=0.5):
 
     def reference(kv, skip_layers=(), fix_kv_size=fix, keep_ratio=keep_ratio):
         out = []
-        for i, (k, v) in enumerate(kv):  # fix_size_l2.py:69-74 skip tests, then :99-150
+        for i, (k, v) in enumerate(kv):  # fix_size_l2.py:69-74 skip tests, then :76-150
             if k.size(2) <= fix_kv_size or i in skip_layers:
                 out.append((k, v))
                 continue
@@ -188,10 +207,15 @@ def ppl_delta(device, arch="pythia-2.8b", tokens=2000, fix=512, keep_ratio=0.5):
         torch.set_default_dtype(prev)
     text = "The quick brown fox jumps over the lazy dog. " * (tokens // 40 + 1)
     kw = dict(fix_kv_size=fix, keep_ratio=keep_ratio)
+    print(f"[bench] PPL-delta leg: {tokens} tokens x 2 runs", file=sys.stderr, flush=True)
     t0 = time.perf_counter()
-    r = [evaluate_with_compression(model, Tok(), text, compress_fn=fn, compress_kwargs=kw,
-                                   max_tokens=tokens, skip_layers=[0, 1], show_progress=False)
-         for fn in (fix_size_l2_compress, reference)]
+    r = []
+    for name, fn in (("engine", fix_size_l2_compress), ("reference", reference)):
+        r.append(evaluate_with_compression(model, Tok(), text, compress_fn=fn, compress_kwargs=kw,
+                                           max_tokens=tokens, skip_layers=[0, 1],
+                                           show_progress=False))
+        print(f"[bench] PPL-delta leg: {name} run done ({time.perf_counter() - t0:.0f} s)",
+              file=sys.stderr, flush=True)
     dt = time.perf_counter() - t0
     del model
     torch.cuda.empty_cache()
@@ -202,7 +226,8 @@ def ppl_delta(device, arch="pythia-2.8b", tokens=2000, fix=512, keep_ratio=0.5):
             "sample": f"fix_size_l2(fix_kv_size={fix}, keep_ratio={keep_ratio}), "
                       f"skip_layers=[0, 1], random-init {arch} architecture (GPT-NeoX) bf16, "
                       f"{r[0]['num_tokens']} synthetic tokens teacher-forced; engine vs the "
-                      f"reference's CPU op sequence as compress_fn ({dt:.0f} s)"}
+                      f"reference's CPU op sequence (golden-pinned port) as compress_fn "
+                      f"({dt:.0f} s)"}
 
 
 def timed_steps(step, steps, warmup, dist, sync, device, on_start=None):
@@ -257,6 +282,43 @@ def capture_jobs(step):
     return seen
 
 
+def _free_port():
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    return port
+
+
+def spawn_ranks(n):
+    """`--gpus N` without a launcher: start N copies of this script as ranks 0..N-1 (one GPU
+    each, LOCAL_RANK = rank) and wait for them.  This process never touches the GPU (importing
+    torch initialises nothing) and never re-execs itself; rank 0 prints the JSON line.  Returns
+    the first non-zero child exit code (the other ranks are then stopped), else 0."""
+    env = dict(os.environ, WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()))
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                              env=dict(env, RANK=str(r), LOCAL_RANK=str(r)))
+             for r in range(n)]
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    for q in procs:  # a failed rank would leave the others in a barrier
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            p.kill()
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -271,53 +333,84 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ppl-model", default="pythia-2.8b", choices=sorted(PPL_MODELS),
                     help="architecture of the random-init model of the PPL-delta leg")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="harness check on CPU: gloo, stand-in step, no engine, no GPU")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if args.dry_run:
+        dev = torch.device("cpu")
+        sync = lambda: None  # noqa: E731
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        sync = torch.cuda.synchronize
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dry_run:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from kvcompress import _engine
     from kvcompress.methods import get_compress_fn
 
     method, kwargs, seq_len, head_dim, what = WORKLOADS[args.workload]
-    if args.layers_total:
-        l0, l1 = shard_layers(args.layers_total, world, rank)
-        total, scaling = args.layers_total, "strong"
+    layers_total = args.layers_total or STRONG_DEFAULT.get(args.workload, 0)
+    if layers_total:
+        l0, l1 = shard_layers(layers_total, world, rank)
+        total, scaling = layers_total, "strong"
     else:  # rank r owns layers [32r, 32r + 32) of a 32*N-layer stack
         l0, l1 = LAYERS * rank, LAYERS * (rank + 1)
         total, scaling = LAYERS * world, "weak"
     n_layers = l1 - l0
-    extra = dict(layer_offset=l0, num_layers_total=total) if method == "pyramid_kv" else {}
+    # global layer ids on every rank: skip_layers (and pyramid_kv's depth-dependent sizes)
+    extra = dict(layer_offset=l0)
+    if method == "pyramid_kv":
+        extra["num_layers_total"] = total
     fn = get_compress_fn(method)
 
-    g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    layers = []
-    for _ in range(n_layers):
-        k = torch.randn(B, H, seq_len, head_dim, device=dev, generator=g,
-                        dtype=torch.float32).to(DTYPES[args.dtype])
-        v = torch.randn(B, H, seq_len, head_dim, device=dev, generator=g,
-                        dtype=torch.float32).to(DTYPES[args.dtype])
-        layers.append((k, v))
+    if args.dry_run:  # stand-in data and step: the harness, not the engine, is under test
+        seq_len, head_dim = 64, 8
+        g = torch.Generator().manual_seed(1000 + rank)
+        layers = [(torch.randn(1, 2, seq_len, head_dim, generator=g),) * 2
+                  for _ in range(n_layers)]
 
-    def step():
-        return fn(layers, skip_layers=[], **kwargs, **extra)
+        def step():
+            time.sleep(0.002 * (rank + 1))  # the last rank is the slow one
+            return [(k[:, :, :8], v[:, :, :8]) for k, v in layers]
+        nbytes = {"path": 1, "score": 1, "select+gather": 1}
+        timer = None
+    else:
+        g = torch.Generator(device=dev).manual_seed(1000 + rank)
+        layers = []
+        for _ in range(n_layers):
+            k = torch.randn(B, H, seq_len, head_dim, device=dev, generator=g,
+                            dtype=torch.float32).to(DTYPES[args.dtype])
+            v = torch.randn(B, H, seq_len, head_dim, device=dev, generator=g,
+                            dtype=torch.float32).to(DTYPES[args.dtype])
+            layers.append((k, v))
 
-    es = layers[0][0].element_size() if layers else 2
-    nbytes = job_bytes(capture_jobs(step), es)
-    # per-kernel durations: the engine splits each launch into its three kernels with HIP
-    # events (recorded on the stream they run on) for the whole timed region
-    timer = _engine.PhaseTimer()
-    elapsed = timed_steps(step, args.steps, args.warmup, dist, torch.cuda.synchronize, dev,
-                          on_start=lambda: _engine.set_phase_timer(timer))
-    _engine.set_phase_timer(None)
-    dur = {k: sum(v) / len(v) for k, v in timer.durations_ms().items()}
+        def step():
+            return fn(layers, skip_layers=[], **kwargs, **extra)
+
+        es = layers[0][0].element_size() if layers else 2
+        nbytes = job_bytes(capture_jobs(step), es)
+        # per-kernel durations: the engine splits each launch into its kernels with HIP events
+        # (recorded on the stream they run on) for the whole timed region
+        timer = _engine.PhaseTimer()
+    elapsed = timed_steps(step, args.steps, args.warmup, dist, sync, dev,
+                          on_start=(lambda: _engine.set_phase_timer(timer)) if timer else None)
+    if timer:
+        _engine.set_phase_timer(None)
+        dur = {k: sum(v) / len(v) for k, v in timer.durations_ms().items()}
+    else:
+        dur = {"score": elapsed / max(args.steps, 1) * 1e3}
 
     # units all ranks processed: positions scored (layers x S) per step
     units = torch.tensor([n_layers * seq_len], dtype=torch.float64)
@@ -331,7 +424,8 @@ def main():
         kern = max(dur, key=dur.get)  # dominant kernel of the step
         kern_gbps = nbytes[kern] / (dur[kern] * 1e-3) / 1e9
         headline = args.workload == HEADLINE
-        traffic = pmc_traffic() if headline and kern == "score" and args.dtype == "bf16" else None
+        traffic = (pmc_traffic() if headline and kern == "score" and args.dtype == "bf16"
+                   and not args.dry_run else None)
         path_gbps = nbytes["path"] * world / (ms_step * 1e-3) / 1e9
         desc = {"score": "score_kernel (key L2 norms)",
                 "select+gather": "select_gather_kernel (selection + segment copy)"}[kern]
@@ -349,7 +443,7 @@ def main():
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic (torch.randn, HBM-resident)",
-            "config": {"workload": f"{method if method.endswith('_compress') else method + '_compress'}({cfg_kw}, skip_layers=[]) over "
+            "config": {"workload": f"{method}_compress({cfg_kw}, skip_layers=[]) over "
                                    f"{n_layers} layers of K,V [1,{H},{seq_len},{head_dim}] per "
                                    f"GPU, one call per step ({what})",
                        "name": args.workload, "layers_per_gpu": n_layers,
@@ -369,7 +463,9 @@ def main():
         }
         ev = sum(kv[0].size(2) for kv in layers) - sum(kv[0].size(2) for kv in step())
         res["tokens_evicted_per_sec"] = ev * world * args.steps / elapsed
-        if not args.no_cpu_baseline and method == "fix_size_l2" and world == 1:  # N=1 only
+        if args.dry_run:
+            res["dry_run"] = True
+        elif not args.no_cpu_baseline and method == "fix_size_l2" and world == 1:  # N=1 only
             res["cpu_baseline"] = cpu_baseline(seq_len, head_dim, dtype=args.dtype)
             res["ppl_delta_vs_ref"] = ppl_delta(dev, arch=args.ppl_model)
         print(json.dumps(res), flush=True)

@@ -17,10 +17,11 @@
 //                   torch.cat of the reference, e.g. fix_size_l2.py:137-147).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
 #include <string.h>
 
+#include <tuple>
 #include <type_traits>
+#include <utility>
 
 #include "kvc.h"
 #include "kvc_common.h"
@@ -140,15 +141,6 @@ __device__ __forceinline__ uint4 canon_nan_dt(uint4 a) {
   } while (0)
 #endif
 
-// threadIdx.x behind an opaque (volatile) move: values derived from it are recomputed where they
-// are used instead of being hoisted out of the fused kernel's persistent loop, where they would
-// stay live (and spill) through the register-hungry select code.
-__device__ __forceinline__ int opaque_tid() {
-  int t = (int)threadIdx.x;
-  asm volatile("" : "+v"(t));
-  return t;
-}
-
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -197,11 +189,10 @@ __host__ __device__ constexpr int score_cp(int nc) { return nc == 4 ? 4 : (nc % 
 
 // One 64-token tile of one (layer, b, h) row: coalesced 16-B loads -> per-wave LDS slab ->
 // one lane per token, torch.norm's 8-accumulator FMA order (fp16: its serial order).  `wl` is
-// this wave's slab (kTile * ROWB bytes).  sc1 = publish the norms write-through for an in-launch consumer.
+// this wave's slab (kTile * ROWB bytes).
 template <int DT, int NC, bool NTL = false>
 __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int tt, int H,
-                                           char* wl, char* norms, int64_t norm_stride,
-                                           bool sc1) {
+                                           char* wl, char* norms, int64_t norm_stride) {
   constexpr int ESZ = DTypeTraits<DT>::esz;
   constexpr int CP = score_cp(NC);  // 16-B chunks per token per phase
   constexpr int NPH = NC / CP;
@@ -258,17 +249,9 @@ __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int t
     char* nrow = norms + (int64_t)(ly->row0 + row) * norm_stride * ESZ;
     if constexpr (DT != KVC_F32) {
       uint16_t* d = reinterpret_cast<uint16_t*>(nrow) + tok0 + lane;
-      const uint16_t val = (uint16_t)bits16_dt<DT>(r);
-      if (sc1)
-        __hip_atomic_store(d, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else
-        *d = val;
+      *d = (uint16_t)bits16_dt<DT>(r);
     } else {
-      float* d = reinterpret_cast<float*>(nrow) + tok0 + lane;
-      if (sc1)
-        __hip_atomic_store(d, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else
-        *d = r;
+      reinterpret_cast<float*>(nrow)[tok0 + lane] = r;
     }
   }
 }
@@ -298,7 +281,7 @@ __global__ void __launch_bounds__(kScoreThreads)
     const int tpr = (ly->zone_len + kTile - 1) / kTile;
     const int local = (int)(g - ly->tile0);
     const int row = local / tpr;
-    score_tile<DT, NC, NTL>(ly, row, local - row * tpr, H, lds[wid], norms, norm_stride, false);
+    score_tile<DT, NC, NTL>(ly, row, local - row * tpr, H, lds[wid], norms, norm_stride);
   }
 }
 
@@ -1339,47 +1322,10 @@ __global__ void __launch_bounds__(kGatherThreads)
 }
 
 // ---------------------------------------------------------------------------------------------
-// FUSED persistent kernel: score, select and gather of a whole call in one launch
+// Row copy shared by the select+gather kernel
 // ---------------------------------------------------------------------------------------------
-// One 1024-thread workgroup per CU.  Each workgroup takes an arrival ticket; the first
-// `n_score_first` arrivals start as SCORE workgroups, the rest go straight to the ROW queue.
-//   SCORE: score wave w (of n_score_first * 16) takes chunks w, w + W, ... of 4 consecutive
-//     64-position tiles (the global layer-major tile order of kvc_plan), computes their norms
-//     (score_tile, write-through stores), drains (`s_waitcnt vmcnt(0)`) and sets the chunk's
-//     per-tile flags with plain write-through stores.  (Agent-scope atomics here cost ~8% of
-//     the stream: a pending atomic makes the wave's next load wait for it.)  Then the
-//     workgroup joins the ROW queue.
-//   ROW: rows are dequeued in layer-major order (the next ticket is fetched while a row runs);
-//     a selecting row polls its tile flags (one load per thread, __syncthreads_and, s_sleep),
-//     then one agent-scope acquire (L1 invalidate), a barrier, select into LDS, gather; a
-//     copy-only row is gathered at once.
-// Progress is guaranteed: tickets are sequential, so once any workgroup is on the ROW queue
-// every SCORE workgroup is resident, and SCORE waves never wait.  Spins are bounded anyway
-// (ctl[kCtlError] = 1).  While the ROW workgroups select (LDS/issue-bound) the SCORE
-// workgroups keep HBM streaming -- the reason to fuse.  (cdna_hip_programming.md §6
-// Guideline 16 for the publish / acquire protocol.)
-constexpr int kChunkTiles = 4;
-// tuning timeline (diag & 2): s_memrealtime (100 MHz, chip-wide) stamps into the idle index region
-#define KVC_TL(slot)                                                   \
-  do {                                                                 \
-    if ((diag & 2) && tid == 0) tl[slot] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-constexpr int kCtlHeader = 32;  // ints before the per-row counters
-constexpr int kCtlTicket = 0, kCtlError = 1, kCtlRowQ = 2;
-
-__host__ __device__ __forceinline__ bool fused_selects(const kvc_layer_t& y) {
+__host__ __device__ __forceinline__ bool layer_selects(const kvc_layer_t& y) {
   return y.n_select > 0 && y.n_select < y.zone_len;
-}
-
-// layer of global score tile g: the largest l with L[l].tile0 <= g (copy-only layers own no
-// tiles and share tile0 with the next layer, so they are never the largest such l for g < total)
-__device__ __forceinline__ const kvc_layer_t* tile_layer(const kvc_layer_t* L, int nl, int g) {
-  int lo = 0, hi = nl - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (L[mid].tile0 <= g) lo = mid; else hi = mid - 1;
-  }
-  return L + lo;
 }
 
 // Copy one output row (sink ++ selected ++ tail) of K and V with the whole workgroup.
@@ -1400,7 +1346,7 @@ __device__ __forceinline__ void gather_row(const kvc_layer_t* __restrict__ ly, i
   const int64_t kss = ly->k_stride[2] * ESZ, vss = ly->v_stride[2] * ESZ;
   char* ko = static_cast<char*>(ly->k_out) + (int64_t)r * nu * 16;
   char* vo = static_cast<char*>(ly->v_out) + (int64_t)r * nu * 16;
-  const int tid0 = opaque_tid();
+  const int tid0 = (int)threadIdx.x;
   for (int u0 = 0; u0 < nu; u0 += NT * BATCH) {
     uint4 xk[BATCH], xv[BATCH];
     bool gat[BATCH];
@@ -1449,111 +1395,6 @@ __device__ __forceinline__ void gather_row(const kvc_layer_t* __restrict__ ly, i
   }
 }
 
-template <int DT, int NC>
-__global__ void __launch_bounds__(kSelThreads)
-    fused_kernel(const kvc_layer_t* __restrict__ L, int nl, int H, int BH, int order, int algo,
-                 char* __restrict__ norms, int64_t norm_stride, int* __restrict__ ctl,
-                 int wave_seg, int total_tiles, int rows, int n_score_first, int diag,
-                 uint64_t* __restrict__ tl) {
-  typedef typename DTypeTraits<DT>::key_t KeyT;
-  constexpr int ESZ = DTypeTraits<DT>::esz;
-  static_assert(NC == 8 || NC == 16, "fused path: 128/256-byte rows");
-  constexpr int ROWB = 8 * 16 + 16;
-  constexpr int SCORE_B = kSelWaves * kTile * ROWB;
-  constexpr int SEL_B = (int)sel_bytes(kZoneMax, (int)sizeof(KeyT), kZoneMax / 2 + 1);
-  constexpr int SM_B = SCORE_B > SEL_B ? SCORE_B : SEL_B;
-  __shared__ __attribute__((aligned(16))) char smem[SM_B];
-  __shared__ SelScalars<KeyT> sc;
-  __shared__ int sh_val;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wid = tid >> 6;
-  int* tile_flag = ctl + kCtlHeader;
-  if (tid == 0)
-    sh_val = __hip_atomic_fetch_add(ctl + kCtlTicket, 1, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  const int ticket = __builtin_amdgcn_readfirstlane(sh_val);
-  __syncthreads();
-  KVC_TL(rows * 4 + ticket * 2);
-
-  if (ticket < n_score_first) {  // ---- SCORE: static chunk striding over the score waves ----
-    char* wl = smem + wid * kTile * ROWB;
-    const int nchunks = (total_tiles + kChunkTiles - 1) / kChunkTiles;
-    const int nsw = n_score_first * kSelWaves;
-    for (int claim = ticket * kSelWaves + wid; claim < nchunks; claim += nsw) {
-      const int g0 = claim * kChunkTiles;
-      const int ng = min(kChunkTiles, total_tiles - g0);
-      for (int i = 0; i < ng; ++i) {
-        const int g = g0 + i;
-        const kvc_layer_t* ly = tile_layer(L, nl, g);
-        const int tpr = (ly->zone_len + kTile - 1) / kTile;
-        const int local = g - ly->tile0;
-        const int row = local / tpr;
-        score_tile<DT, NC, true>(ly, row, local - row * tpr, H, wl, norms, norm_stride, true);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // norms reach L2 before the flags
-      if (lane < ng)
-        __hip_atomic_store(tile_flag + g0 + lane, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  if (diag & 5) return;  // tuning: score phase alone (4: on the cus - nsel score workgroups)
-  __syncthreads();
-  KVC_TL(rows * 4 + ticket * 2 + 1);
-
-  // ---- ROW queue: select + gather; the next row's ticket is fetched while this one runs ----
-  if (tid == 0)
-    sh_val = __hip_atomic_fetch_add(ctl + kCtlRowQ, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  int r = __builtin_amdgcn_readfirstlane(sh_val);
-  __syncthreads();
-  int next = 0;
-  while (r < rows) {
-    if (tid == 0)
-      next = __hip_atomic_fetch_add(ctl + kCtlRowQ, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    KVC_TL(r * 4);
-    const int l = r / BH;
-    const kvc_layer_t* ly = L + l;
-    const int row = r - l * BH;
-    if (fused_selects(*ly)) {
-      const int tpr = (ly->zone_len + kTile - 1) / kTile;
-      const int* f = tile_flag + ly->tile0 + row * tpr;
-      for (int spins = 0;; ++spins) {  // every tile of the row flagged?
-        int ok = 1;
-        for (int t = tid; t < tpr; t += kSelThreads)
-          ok &= __hip_atomic_load(f + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__syncthreads_and(ok)) break;
-        if (spins > (1 << 22)) {
-          if (tid == 0)
-            __hip_atomic_store(ctl + kCtlError, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(8);
-      }
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __syncthreads();
-      KVC_TL(r * 4 + 1);
-      uint16_t* sel = reinterpret_cast<uint16_t*>(smem);  // key region, dead after the chain
-      select_body<DT, true, kZoneMax, kSelThreads>(ly, order, algo,
-                                                   norms + (int64_t)r * norm_stride * ESZ, nullptr,
-                                                   sel, smem, kZoneMax, kZoneMax / 2 + 1, sc,
-                                                   wave_seg, nullptr);
-      __syncthreads();
-      KVC_TL(r * 4 + 2);
-      gather_row<DT, NC>(ly, row, H, sel);
-    } else {
-      gather_row<DT, NC>(ly, row, H, nullptr);
-    }
-    if (tid == 0) sh_val = next;
-    __syncthreads();  // LDS and sh_val are reused by the next row
-    KVC_TL(r * 4 + 3);
-    r = __builtin_amdgcn_readfirstlane(sh_val);
-    __syncthreads();
-  }
-}
-
 // ---------------------------------------------------------------------------------------------
 // SELECT + GATHER: one workgroup per (layer, b, h) row selects into LDS and copies the row's
 // output (sink ++ selected ++ tail of K and V) straight from the LDS index list.  With two
@@ -1573,7 +1414,7 @@ __global__ void __launch_bounds__(NT, 8)
   const kvc_layer_t* ly = T.l + blockIdx.x / BH;
   const int r = (int)(blockIdx.x % BH);
   if (ly->n_out == 0) return;
-  const bool selects = fused_selects(*ly);
+  const bool selects = layer_selects(*ly);
   const char* nrow = norms + (int64_t)(ly->row0 + r) * norm_stride * ESZ;
   char* arrays;
   if constexpr (NT == kSelThreads) {
@@ -1600,13 +1441,10 @@ __global__ void __launch_bounds__(NT, 8)
 static inline int esize(int dtype) { return dtype == KVC_F32 ? 4 : 2; }
 // Calls f(std::integral_constant<int, DT>) for the call's storage dtype (validated by plan_impl).
 template <typename F>
-static void with_dtype(int dtype, F&& f) {
-  if (dtype == KVC_BF16)
-    f(std::integral_constant<int, KVC_BF16>());
-  else if (dtype == KVC_F16)
-    f(std::integral_constant<int, KVC_F16>());
-  else
-    f(std::integral_constant<int, KVC_F32>());
+static int with_dtype(int dtype, F&& f) {
+  if (dtype == KVC_BF16) return f(std::integral_constant<int, KVC_BF16>());
+  if (dtype == KVC_F16) return f(std::integral_constant<int, KVC_F16>());
+  return f(std::integral_constant<int, KVC_F32>());
 }
 static inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
@@ -1680,10 +1518,6 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
     info->norm_row_stride = (int64_t)round_up((size_t)max_zone, kTile);
     info->index_row_stride = (int64_t)round_up((size_t)(max_sel > 0 ? max_sel : 1), 16);
     size_t off = 0;
-    info->control_offset = off;  // fused kernel: tickets, error flag, row queue, tile flags
-    off = round_up(off + (size_t)(kCtlHeader + tiles) * 4, 256);
-    info->desc_offset = off;
-    off = round_up(off + (size_t)nl * sizeof(kvc_layer_t), 256);
     info->norm_offset = off;
     off = round_up(off + (size_t)rows * info->norm_row_stride * es, 256);
     info->index_offset = off;
@@ -1698,83 +1532,129 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
   return KVC_OK;
 }
 
+// Every launch goes through hipLaunchKernel, whose return value is this launch's own status (a
+// caller's pending HIP error is neither consumed nor reported as ours).
+template <typename... P, typename... A>
+static int launch_k(void (*kern)(P...), dim3 grid, dim3 block, size_t lds, hipStream_t s,
+                    A&&... a) {
+  std::tuple<P...> args(std::forward<A>(a)...);
+  void* ptrs[sizeof...(P)];
+  std::apply([&](auto&... x) {
+    int i = 0;
+    ((ptrs[i++] = static_cast<void*>(&x)), ...);
+  }, args);
+  return hipLaunchKernel(reinterpret_cast<const void*>(kern), grid, block, ptrs, lds, s) ==
+                 hipSuccess
+             ? KVC_OK
+             : KVC_E_HIP;
+}
+
+// Calls f(std::integral_constant<int, NC>()) for a row width in 16-B chunks (validated by
+// plan_impl: 64..1024-byte rows).
+template <typename F>
+static int with_nc(int nc, F&& f) {
+  switch (nc) {
+    case 4: return f(std::integral_constant<int, 4>());
+    case 8: return f(std::integral_constant<int, 8>());
+    case 10: return f(std::integral_constant<int, 10>());
+    case 16: return f(std::integral_constant<int, 16>());
+    case 20: return f(std::integral_constant<int, 20>());
+    case 32: return f(std::integral_constant<int, 32>());
+    case 64: return f(std::integral_constant<int, 64>());
+    default: return KVC_E_HEADDIM;
+  }
+}
+
+// Keys are read once (non-temporal loads) and outputs written once (non-temporal stores): they
+// would otherwise evict useful lines from the Infinity Cache.
 template <int DT, int NC>
-static void launch_score(const LayerChunk& T, int nl, int H, int64_t tile_base,
-                         int64_t chunk_tiles, char* norms, int64_t nstride, hipStream_t s) {
-  unsigned grid = (unsigned)((chunk_tiles + kScoreWaves - 1) / kScoreWaves);
-  // tuning only: a persistent grid of KVC_SCORE_GRID workgroups (waves stride over the tiles)
-  if (const char* e = getenv("KVC_SCORE_GRID"))
-    if (atoi(e) > 0 && (unsigned)atoi(e) < grid) grid = (unsigned)atoi(e);
-  const char* ntl = getenv("KVC_SCORE_NT");  // keys are read once: non-temporal by default
-  if (!(ntl && strcmp(ntl, "0") == 0))
-    hipLaunchKernelGGL((score_kernel<DT, NC, true>), dim3(grid), dim3(kScoreThreads), 0, s, T,
-                       nl, H, tile_base, chunk_tiles, norms, nstride);
-  else
-    hipLaunchKernelGGL((score_kernel<DT, NC, false>), dim3(grid), dim3(kScoreThreads), 0, s, T,
-                       nl, H, tile_base, chunk_tiles, norms, nstride);
+static int launch_score(const LayerChunk& T, int nl, int H, int64_t tile_base,
+                        int64_t chunk_tiles, char* norms, int64_t nstride, hipStream_t s) {
+  const unsigned grid = (unsigned)((chunk_tiles + kScoreWaves - 1) / kScoreWaves);
+  return launch_k(score_kernel<DT, NC, true>, dim3(grid), dim3(kScoreThreads), 0, s, T, nl, H,
+                  tile_base, chunk_tiles, norms, nstride);
 }
 
 // `work` = max n_out over the chunk's layers; grid = (rows, token blocks)
 template <int DT, int NC>
-static void launch_gather(const LayerChunk& T, int nl, int H, int BH, const int32_t* idx,
-                          int64_t istride, int64_t work, hipStream_t s) {
+static int launch_gather(const LayerChunk& T, int nl, int H, int BH, const int32_t* idx,
+                         int64_t istride, int64_t work, hipStream_t s) {
   const dim3 grid((unsigned)(nl * BH), (unsigned)((work + kGatherTokens - 1) / kGatherTokens));
-  const char* nts = getenv("KVC_GATHER_NT");  // outputs are written once: non-temporal default
-  if (!(nts && strcmp(nts, "0") == 0))
-    hipLaunchKernelGGL((gather_kernel<DT, NC, true>), grid, dim3(kGatherThreads), 0, s, T, H, BH,
-                       idx, istride);
-  else
-    hipLaunchKernelGGL((gather_kernel<DT, NC, false>), grid, dim3(kGatherThreads), 0, s, T, H,
-                       BH, idx, istride);
+  return launch_k(gather_kernel<DT, NC, true>, grid, dim3(kGatherThreads), 0, s, T, H, BH, idx,
+                  istride);
 }
 
-template <int DT>
-static void dispatch_nc(int nc, bool score, const LayerChunk& T, int nl, int H, int BH,
-                        int64_t base, int64_t work, char* norms, int64_t nstride,
-                        const int32_t* idx, int64_t istride, hipStream_t s) {
-#define KVC_NC_CASE(NCV)                                                   \
-  case NCV:                                                                \
-    if (score)                                                             \
-      launch_score<DT, NCV>(T, nl, H, base, work, norms, nstride, s);      \
-    else                                                                   \
-      launch_gather<DT, NCV>(T, nl, H, BH, idx, istride, work, s);         \
-    break;
-  switch (nc) {
-    KVC_NC_CASE(4)
-    KVC_NC_CASE(8)
-    KVC_NC_CASE(10)
-    KVC_NC_CASE(16)
-    KVC_NC_CASE(20)
-    KVC_NC_CASE(32)
-    KVC_NC_CASE(64)
-    default:
-      break;
+// One chunk of <= kArgLayers layers: SCORE, then SELECT_GATHER (or SELECT and GATHER as two
+// kernels with KVC_FLAG_SPLIT_SELECT_GATHER, or GATHER alone for copy-only / external-index
+// calls), each kernel with the chunk's table by value.
+template <int DT, int NC>
+static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, const kvc_layer_t* layers,
+                        int nl, int c0, int cn, char* w, hipStream_t s) {
+  typedef typename DTypeTraits<DT>::key_t KeyT;
+  const int H = p->heads, BH = p->batch * p->heads;
+  char* norms = w + info.norm_offset;
+  int32_t* idx = reinterpret_cast<int32_t*>(w + info.index_offset);
+  const int64_t nstride = info.norm_row_stride, istride = info.index_row_stride;
+#ifdef KVC_STAMPS
+  uint64_t* stamps = reinterpret_cast<uint64_t*>(w + info.workspace_bytes - info.rows * 256);
+#else
+  uint64_t* stamps = nullptr;
+#endif
+  LayerChunk T;
+  memcpy(T.l, layers + c0, (size_t)cn * sizeof(kvc_layer_t));
+  const int64_t tile_base = layers[c0].tile0;
+  const int64_t tile_end = c0 + cn < nl ? (int64_t)layers[c0 + cn].tile0 : info.score_tiles;
+  bool sel = false, long_zone = false;
+  int64_t max_out = 0;
+  for (int l = c0; l < c0 + cn; ++l) {
+    sel |= layers[l].n_select > 0;
+    long_zone |= layer_selects(layers[l]) && layers[l].zone_len > kZoneMax;
+    max_out = layers[l].n_out > max_out ? layers[l].n_out : max_out;
   }
-#undef KVC_NC_CASE
-}
-
-template <int DT, int NT>
-static void launch_select_gather(int nc, const LayerChunk& T, int nl, int H, int BH, int order,
-                                 int algo, const char* norms, int64_t nstride, int wave_seg,
-                                 int n_cap, int cap, size_t lds, hipStream_t s) {
-  const dim3 grid((unsigned)(nl * BH));
-#define KVC_SG_CASE(NCV)                                                                    \
-  case NCV:                                                                                 \
-    hipLaunchKernelGGL((select_gather_kernel<DT, NT, NCV>), grid, dim3(NT), lds, s, T, H, BH, \
-                       order, algo, norms, nstride, wave_seg, n_cap, cap);                  \
-    break;
-  switch (nc) {
-    KVC_SG_CASE(4)
-    KVC_SG_CASE(8)
-    KVC_SG_CASE(10)
-    KVC_SG_CASE(16)
-    KVC_SG_CASE(20)
-    KVC_SG_CASE(32)
-    KVC_SG_CASE(64)
-    default:
-      break;
+  const bool ext = p->external_index != 0;
+  int rc = KVC_OK;
+  if ((p->phases & KVC_PHASE_SCORE) && tile_end > tile_base && !ext)
+    rc = launch_score<DT, NC>(T, cn, H, tile_base, tile_end - tile_base, norms, nstride, s);
+  if (rc != KVC_OK) return rc;
+  const dim3 rows_grid((unsigned)(cn * BH));
+  const int n_cap = (int)nstride;  // longest zone of the call, rounded to 64
+  if ((p->phases & KVC_PHASE_SELECT) && sel && !ext && long_zone) {
+    char* scratch = w + round_up(info.index_offset + (size_t)info.rows * istride * 4, 256);
+    const int64_t rb = (int64_t)sel_scratch_row_bytes(n_cap, p->dtype);
+    if (n_cap > kZoneMaxGlobal)  // u32 positions (the call's longest zone decides)
+      rc = launch_k(select_long_kernel<DT>, rows_grid, dim3(kSelThreads), 0, s, T, BH, p->order,
+                    p->algo, norms, nstride, idx, istride, scratch, rb, n_cap);
+    else
+      rc = launch_k(select_global_kernel<DT>, rows_grid, dim3(kSelThreads), 0, s, T, BH,
+                    p->order, p->algo, norms, nstride, idx, istride, kWaveSeg, scratch, rb, n_cap);
+  } else if ((p->phases & KVC_PHASE_SELECT) && sel && !ext) {
+    uint64_t* st = stamps ? stamps + (size_t)layers[c0].row0 * 32 : nullptr;
+    const int ks = (int)sizeof(KeyT);
+    const bool small = n_cap <= kSmallZone;
+    const int cap = small ? sel_cap(n_cap, ks) : 0;
+    const size_t lds = small ? sel_bytes(n_cap, ks, cap) : 0;
+    const bool fuse_sg = (p->phases & KVC_PHASE_GATHER) && max_out > 0 && !stamps &&
+                         !(p->flags & KVC_FLAG_SPLIT_SELECT_GATHER);
+    if (fuse_sg) {  // this chunk's gather happens inside the select kernel
+      if (small)
+        return launch_k(select_gather_kernel<DT, kSelThreadsSmall, NC>, rows_grid,
+                        dim3(kSelThreadsSmall), lds, s, T, H, BH, p->order, p->algo, norms,
+                        nstride, kWaveSeg, n_cap, cap);
+      return launch_k(select_gather_kernel<DT, kSelThreads, NC>, rows_grid, dim3(kSelThreads),
+                      lds, s, T, H, BH, p->order, p->algo, norms, nstride, kWaveSeg, n_cap, cap);
+    }
+    if (small)
+      rc = launch_k(select_kernel<DT, kSelThreadsSmall>, rows_grid, dim3(kSelThreadsSmall), lds,
+                    s, T, BH, p->order, p->algo, norms, nstride, idx, istride, kWaveSeg, n_cap,
+                    cap, st);
+    else
+      rc = launch_k(select_kernel<DT, kSelThreads>, rows_grid, dim3(kSelThreads), lds, s, T, BH,
+                    p->order, p->algo, norms, nstride, idx, istride, kWaveSeg, n_cap, cap, st);
   }
-#undef KVC_SG_CASE
+  if (rc != KVC_OK) return rc;
+  if ((p->phases & KVC_PHASE_GATHER) && max_out > 0)
+    rc = launch_gather<DT, NC>(T, cn, H, BH, idx, istride, max_out, s);
+  return rc;
 }
 
 }  // namespace kvc
@@ -1804,8 +1684,8 @@ int kvc_plan(const kvc_params_t* params, kvc_layer_t* layers, int num_layers,
   return kvc::plan_impl(params, layers, num_layers, info, true);
 }
 
-int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer_t* layers_dev,
-               int nl, void* ws, size_t ws_bytes, kvc_stream_t stream) {
+int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, int nl, void* ws,
+               size_t ws_bytes, kvc_stream_t stream) {
   using namespace kvc;
   kvc_plan_info_t info;
   int rc = plan_impl(p, const_cast<kvc_layer_t*>(layers), nl, &info, false);
@@ -1814,153 +1694,17 @@ int kvc_launch(const kvc_params_t* p, const kvc_layer_t* layers, const kvc_layer
   if (!ws || ws_bytes < info.workspace_bytes) return KVC_E_WORKSPACE;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   char* w = static_cast<char*>(ws);
-  const int es = esize(p->dtype);
-  const int nc = p->head_dim * es / 16;
-  const int H = p->heads;
-  const int BH = p->batch * p->heads;
-  char* norms = w + info.norm_offset;
-  int32_t* idx = reinterpret_cast<int32_t*>(w + info.index_offset);
-  // wave hand-off threshold (<= 1024: the wave chain covers 64 lanes x 16 positions);
-  // KVC_WAVE_SEG overrides it for tuning sweeps
-  int wave_seg = kWaveSeg;
-  if (const char* e = getenv("KVC_WAVE_SEG")) wave_seg = atoi(e);
-  if (wave_seg < 16) wave_seg = 16;
-  if (wave_seg > 1024) wave_seg = 1024;
-#ifdef KVC_STAMPS
-  uint64_t* stamps = reinterpret_cast<uint64_t*>(w + info.workspace_bytes - info.rows * 256);
-#else
-  uint64_t* stamps = nullptr;
-#endif
-  (void)hipGetLastError();
-  // Fused persistent path (opt-in, KVC_FUSED=1): all phases, no caller-provided indices,
-  // 128/256-byte rows (wider rows need more than the 128 VGPRs a 1024-thread workgroup allows).
-  // It overlaps selection with the key stream, but on the headline workload the three-kernel
-  // path with non-temporal streams is faster, so that is the default.
-  bool fused = p->phases == KVC_PHASE_ALL && !p->external_index && (nc == 8 || nc == 16) &&
-               info.norm_row_stride <= kZoneMax;  // LDS-resident selection only
-  const char* fe = getenv("KVC_FUSED");
-  fused = fused && fe && strcmp(fe, "1") == 0;
-  if (fused) {
-    if (!layers_dev) {  // the persistent kernel reads the whole table from device memory
-      if (hipMemcpyAsync(w + info.desc_offset, layers, (size_t)nl * sizeof(kvc_layer_t),
-                         hipMemcpyHostToDevice, s) != hipSuccess)
-        return KVC_E_HIP;
-      layers_dev = reinterpret_cast<const kvc_layer_t*>(w + info.desc_offset);
-    }
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus <= 0)
-      return KVC_E_HIP;
-    int* ctl = reinterpret_cast<int*>(w + info.control_offset);
-    if (hipMemsetAsync(ctl, 0, (size_t)(kCtlHeader + info.score_tiles) * 4, s) != hipSuccess)
-      return KVC_E_HIP;
-    // Workgroups that start on the ROW queue: enough select throughput to keep pace with the
-    // key stream (select ~7 cycles/position/CU vs ~24 (256-B rows) or ~12 (128-B rows) cycles
-    // of HBM share per position per CU); KVC_SEL_WGS overrides.
-    int nsel = (int)(cus * (nc == 16 ? 0.22 : 0.36) + 0.5);
-    if (const char* e = getenv("KVC_SEL_WGS")) nsel = atoi(e);
-    if (nsel < 1) nsel = 1;
-    if (nsel > cus - 1) nsel = cus - 1;
-    int diag = 0;  // tuning only: 1 = score phase alone (output incomplete)
-    if (const char* e = getenv("KVC_FUSED_DIAG")) diag = atoi(e);
-    const int n_score_first = info.score_tiles > 0 ? cus - ((diag & 1) ? 0 : nsel) : 0;
-    uint64_t* tl = reinterpret_cast<uint64_t*>(idx);
-    if ((diag & 2) && (size_t)info.rows * info.index_row_stride * 4 < (size_t)(info.rows * 4 + 2 * cus) * 8)
-      diag &= ~2;
-    const dim3 grid((unsigned)cus), block(kSelThreads);
-#define KVC_FUSED_LAUNCH(DT_, NC_)                                                             \
-  hipLaunchKernelGGL((fused_kernel<DT_, NC_>), grid, block, 0, s, layers_dev, nl, H, BH,       \
-                     p->order, p->algo, norms, info.norm_row_stride, ctl, wave_seg,             \
-                     (int)info.score_tiles, (int)info.rows, n_score_first, diag, tl)
-    with_dtype(p->dtype, [&](auto dt) {
-      constexpr int DT = decltype(dt)::value;
-      if (nc == 8) { KVC_FUSED_LAUNCH(DT, 8); } else { KVC_FUSED_LAUNCH(DT, 16); }
-    });
-#undef KVC_FUSED_LAUNCH
-    return hipGetLastError() == hipSuccess ? KVC_OK : KVC_E_HIP;
-  }
-  // Three kernels per chunk of <= kArgLayers layers, each with the chunk's table by value.
-  for (int c0 = 0; c0 < nl; c0 += kArgLayers) {
+  const int nc = p->head_dim * esize(p->dtype) / 16;
+  for (int c0 = 0; c0 < nl && rc == KVC_OK; c0 += kArgLayers) {
     const int cn = nl - c0 < kArgLayers ? nl - c0 : kArgLayers;
-    LayerChunk T;
-    memcpy(T.l, layers + c0, (size_t)cn * sizeof(kvc_layer_t));
-    const int64_t tile_base = layers[c0].tile0;
-    const int64_t tile_end = c0 + cn < nl ? (int64_t)layers[c0 + cn].tile0 : info.score_tiles;
-    bool sel = false, long_zone = false;
-    int64_t max_out = 0;
-    for (int l = c0; l < c0 + cn; ++l) {
-      sel |= layers[l].n_select > 0;
-      long_zone |= layers[l].n_select > 0 && layers[l].n_select < layers[l].zone_len &&
-                   layers[l].zone_len > kZoneMax;
-      max_out = layers[l].n_out > max_out ? layers[l].n_out : max_out;
-    }
-    if ((p->phases & KVC_PHASE_SCORE) && tile_end > tile_base && !p->external_index) {
-      with_dtype(p->dtype, [&](auto dt) {
-        dispatch_nc<decltype(dt)::value>(nc, true, T, cn, H, BH, tile_base, tile_end - tile_base,
-                                         norms, info.norm_row_stride, idx, info.index_row_stride,
-                                         s);
+    rc = with_dtype(p->dtype, [&](auto dt) {
+      return with_nc(nc, [&](auto ncv) {
+        return launch_chunk<decltype(dt)::value, decltype(ncv)::value>(p, info, layers, nl, c0,
+                                                                       cn, w, s);
       });
-    }
-    if ((p->phases & KVC_PHASE_SELECT) && sel && !p->external_index && long_zone) {
-      const dim3 grid((unsigned)(cn * BH)), block(kSelThreads);
-      const int n_cap = (int)info.norm_row_stride;
-      char* scratch = w + round_up(info.index_offset +
-                                   (size_t)info.rows * info.index_row_stride * 4, 256);
-      const int64_t rb = (int64_t)sel_scratch_row_bytes(n_cap, p->dtype);
-      with_dtype(p->dtype, [&](auto dt) {
-        if (n_cap > kZoneMaxGlobal)  // u32 positions (the call's longest zone decides)
-          hipLaunchKernelGGL(select_long_kernel<decltype(dt)::value>, grid, block, 0, s, T, BH,
-                             p->order, p->algo, norms, info.norm_row_stride, idx,
-                             info.index_row_stride, scratch, rb, n_cap);
-        else
-          hipLaunchKernelGGL(select_global_kernel<decltype(dt)::value>, grid, block, 0, s, T, BH,
-                             p->order, p->algo, norms, info.norm_row_stride, idx,
-                             info.index_row_stride, wave_seg, scratch, rb, n_cap);
-      });
-    } else if ((p->phases & KVC_PHASE_SELECT) && sel && !p->external_index) {
-      uint64_t* st = stamps ? stamps + (size_t)layers[c0].row0 * 32 : nullptr;
-      const int n_cap = (int)info.norm_row_stride;  // longest zone of the call, rounded to 64
-      const int ks = esize(p->dtype);
-      const char* ent = getenv("KVC_SEL_NT");  // tuning only: 1024 = no small variant
-      const bool small = n_cap <= kSmallZone && !(ent && atoi(ent) == 1024);
-      const int cap = small ? sel_cap(n_cap, ks) : 0;
-      const size_t lds = small ? sel_bytes(n_cap, ks, cap) : 0;
-      // SELECT + GATHER in one kernel when both phases run (KVC_SEL_GATHER=0: separate kernels)
-      const char* esg = getenv("KVC_SEL_GATHER");
-      const bool fuse_sg = (p->phases & KVC_PHASE_GATHER) && max_out > 0 && !stamps &&
-                           !(esg && strcmp(esg, "0") == 0);
-      if (fuse_sg) {
-#define KVC_SG(DT_, NT_)                                                                      \
-  launch_select_gather<DT_, NT_>(nc, T, cn, H, BH, p->order, p->algo, norms,                   \
-                                 info.norm_row_stride, wave_seg, n_cap, cap, lds, s)
-        with_dtype(p->dtype, [&](auto dt) {
-          constexpr int DT = decltype(dt)::value;
-          if (small) KVC_SG(DT, kSelThreadsSmall); else KVC_SG(DT, kSelThreads);
-        });
-#undef KVC_SG
-        continue;  // this chunk's gather is done
-      }
-      const dim3 grid((unsigned)(cn * BH));
-#define KVC_SEL_LAUNCH(DT_, NT_)                                                              \
-  hipLaunchKernelGGL((select_kernel<DT_, NT_>), grid, dim3(NT_), lds, s, T, BH, p->order,    \
-                     p->algo, norms, info.norm_row_stride, idx, info.index_row_stride,       \
-                     wave_seg, n_cap, cap, st)
-      with_dtype(p->dtype, [&](auto dt) {
-        constexpr int DT = decltype(dt)::value;
-        if (small) KVC_SEL_LAUNCH(DT, kSelThreadsSmall);
-        else KVC_SEL_LAUNCH(DT, kSelThreads);
-      });
-#undef KVC_SEL_LAUNCH
-    }
-    if ((p->phases & KVC_PHASE_GATHER) && max_out > 0) {
-      with_dtype(p->dtype, [&](auto dt) {
-        dispatch_nc<decltype(dt)::value>(nc, false, T, cn, H, BH, 0, max_out, norms,
-                                         info.norm_row_stride, idx, info.index_row_stride, s);
-      });
-    }
+    });
   }
-  return hipGetLastError() == hipSuccess ? KVC_OK : KVC_E_HIP;
+  return rc;
 }
 
 int kvc_compress(const kvc_params_t* params, kvc_layer_t* layers, int num_layers, void* ws,
@@ -1968,7 +1712,7 @@ int kvc_compress(const kvc_params_t* params, kvc_layer_t* layers, int num_layers
   kvc_plan_info_t info;
   const int rc = kvc::plan_impl(params, layers, num_layers, &info, true);
   if (rc != KVC_OK) return rc;
-  return kvc_launch(params, layers, nullptr, num_layers, ws, ws_bytes, stream);
+  return kvc_launch(params, layers, num_layers, ws, ws_bytes, stream);
 }
 
 }  // extern "C"

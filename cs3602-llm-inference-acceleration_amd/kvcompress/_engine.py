@@ -69,6 +69,10 @@ class PhaseTimer:
 
 _timer = None
 
+# Launch-path switch for tests and tools: False = SCORE + SELECT_GATHER kernels (default), True =
+# SCORE, SELECT and GATHER as three kernels (kvc_params.flags KVC_FLAG_SPLIT_SELECT_GATHER).
+split_select_gather = False
+
 
 def set_phase_timer(t):
     global _timer
@@ -118,8 +122,7 @@ def execute(jobs: List[Segments], out_list: list, order: int, algo: int):
 
 def _upload(params, table, device, js, B, H):
     """Plan one table and allocate its workspace.  The table itself travels in the kernels'
-    arguments (the library copies it to the workspace only for the opt-in fused kernel);
-    caller-provided indices (strategy="random") are copied into the index region here."""
+    arguments; caller-provided indices (strategy="random") are copied into the index region here."""
     rc, info = N.plan(params, table)
     N.check(rc, "kvc_plan")
     ws = torch.empty(max(int(info.workspace_bytes), 256), dtype=torch.uint8, device=device)
@@ -135,7 +138,6 @@ def _upload(params, table, device, js, B, H):
 
 
 def _launch(params, table, ws, info, stream, phases):
-    dev_tbl = 0  # NULL: by-value tables (the library uploads one itself if it needs it)
     saved = params.phases
     steps = _timer.steps if _timer is not None and _timer.split else (("all", phases),)
     for name, bits in steps:
@@ -145,7 +147,7 @@ def _launch(params, table, ws, info, stream, phases):
         if _timer is not None:
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(stream)
-        rc = N.launch(params, table, dev_tbl, ws.data_ptr(), int(info.workspace_bytes),
+        rc = N.launch(params, table, ws.data_ptr(), int(info.workspace_bytes),
                       stream.cuda_stream)
         if _timer is not None:
             b.record(stream)
@@ -200,7 +202,8 @@ def _run_group(device, dtype, B, H, D, js, out_list, order, algo):
     def params():
         return N.Params(dtype=_SUPPORTED[dtype], batch=B, heads=H, head_dim=D, order=order,
                         algo=algo, phases=N.PHASE_GATHER if external else N.PHASE_ALL,
-                        external_index=1 if external else 0)
+                        external_index=1 if external else 0,
+                        flags=N.FLAG_SPLIT_SELECT_GATHER if split_select_gather else 0)
 
     # One launch (score, select, gather kernels) for every layer of the group.  (Pipelining
     # layer chunks over two streams -- score of chunk c+1 beside select of chunk c -- was

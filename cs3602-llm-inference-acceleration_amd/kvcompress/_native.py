@@ -18,6 +18,8 @@ KVC_ASC, KVC_DESC = 0, 1
 KVC_ALGO_SORT, KVC_ALGO_TOPK = 0, 1
 KVC_SCORE_NORM, KVC_SCORE_SNAPKV = 0, 1
 PHASE_SCORE, PHASE_SELECT, PHASE_GATHER, PHASE_ALL = 1, 2, 4, 7
+FLAG_SPLIT_SELECT_GATHER = 1
+ABI_VERSION = 2
 KVC_E_TOO_LONG = -5
 
 # struct kvc_layer (include/kvc.h) -- 136 bytes, checked against kvc_layer_struct_size()
@@ -35,12 +37,12 @@ assert LAYER_DTYPE.itemsize == 136
 class Params(ctypes.Structure):
     _fields_ = [("dtype", ctypes.c_int32), ("batch", ctypes.c_int32), ("heads", ctypes.c_int32),
                 ("head_dim", ctypes.c_int32), ("order", ctypes.c_int32), ("algo", ctypes.c_int32),
-                ("phases", ctypes.c_int32), ("external_index", ctypes.c_int32)]
+                ("phases", ctypes.c_int32), ("external_index", ctypes.c_int32),
+                ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class PlanInfo(ctypes.Structure):
-    _fields_ = [("control_offset", ctypes.c_size_t),
-                ("desc_offset", ctypes.c_size_t), ("norm_offset", ctypes.c_size_t),
+    _fields_ = [("norm_offset", ctypes.c_size_t),
                 ("index_offset", ctypes.c_size_t), ("workspace_bytes", ctypes.c_size_t),
                 ("norm_row_stride", ctypes.c_int64), ("index_row_stride", ctypes.c_int64),
                 ("rows", ctypes.c_int64), ("score_tiles", ctypes.c_int64),
@@ -76,10 +78,10 @@ def lib():
     L.kvc_plan.restype = i32
     L.kvc_plan.argtypes = [ctypes.POINTER(Params), vp, i32, ctypes.POINTER(PlanInfo)]
     L.kvc_launch.restype = i32
-    L.kvc_launch.argtypes = [ctypes.POINTER(Params), vp, vp, i32, vp, ctypes.c_size_t, vp]
+    L.kvc_launch.argtypes = [ctypes.POINTER(Params), vp, i32, vp, ctypes.c_size_t, vp]
     L.kvc_compress.restype = i32
     L.kvc_compress.argtypes = [ctypes.POINTER(Params), vp, i32, vp, ctypes.c_size_t, vp]
-    if L.kvc_version() != 1 or L.kvc_layer_struct_size() != LAYER_DTYPE.itemsize:
+    if L.kvc_version() != ABI_VERSION or L.kvc_layer_struct_size() != LAYER_DTYPE.itemsize:
         raise NativeLibraryError("libkvc.so ABI mismatch; rebuild it")
     _lib = L
     return L
@@ -100,6 +102,6 @@ def plan(params, table):
     return rc, info
 
 
-def launch(params, table, table_dev_ptr, ws_ptr, ws_bytes, stream_ptr):
-    return lib().kvc_launch(ctypes.byref(params), table.ctypes.data, table_dev_ptr, len(table),
-                            ws_ptr, ws_bytes, stream_ptr)
+def launch(params, table, ws_ptr, ws_bytes, stream_ptr):
+    return lib().kvc_launch(ctypes.byref(params), table.ctypes.data, len(table), ws_ptr, ws_bytes,
+                            stream_ptr)

@@ -9,7 +9,7 @@ import torch
 
 from .. import _engine as E
 from .. import _native as N
-from ..utils import normalize_kv_cache
+from ..utils import layer_offset, normalize_kv_cache
 
 
 def adaptive_l2_compress(
@@ -23,12 +23,13 @@ def adaptive_l2_compress(
     **kwargs
 ) -> List[Tuple[torch.Tensor, torch.Tensor]]:
     past_key_values = list(normalize_kv_cache(past_key_values))
+    offset = layer_offset(kwargs)  # global index of layer 0 (layer-sharded callers)
     if not past_key_values:
         return past_key_values
     jobs = []
     for layer_idx, (keys, values) in enumerate(past_key_values):
         seq_len = keys.size(2)
-        if layer_idx in skip_layers:                                  # :71 (before length test)
+        if layer_idx + offset in skip_layers:                         # :71 (before length test)
             continue
         if seq_len <= soft_limit:
             continue

@@ -10,7 +10,7 @@ import torch
 
 from .. import _engine as E
 from .. import _native as N
-from ..utils import normalize_kv_cache
+from ..utils import layer_offset, normalize_kv_cache
 
 
 def fix_size_l2_compress(
@@ -22,12 +22,13 @@ def fix_size_l2_compress(
     **kwargs
 ) -> List[Tuple[torch.Tensor, torch.Tensor]]:
     past_key_values = list(normalize_kv_cache(past_key_values))
+    offset = layer_offset(kwargs)  # global index of layer 0 (layer-sharded callers)
     jobs = []
     for layer_idx, (keys, values) in enumerate(past_key_values):
         seq_len = keys.size(2)
         if seq_len <= fix_kv_size:                                    # :69
             continue
-        if layer_idx in skip_layers:                                  # :73
+        if layer_idx + offset in skip_layers:                         # :73
             continue
         batch_size, num_heads, seq_len, head_dim = keys.shape
         protected_length = int(fix_kv_size * keep_ratio)              # :79

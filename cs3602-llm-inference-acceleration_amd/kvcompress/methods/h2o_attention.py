@@ -138,7 +138,7 @@ def h2o_attention_compress(past_key_values, attention_scores: Optional[Tuple] = 
 
 
 def create_h2o_manager_from_model(model, **kwargs) -> H2OAttentionManager:
-    """h2o_attention.py:379-404"""
+    """h2o_attention.py:366-391"""
     config = model.config
     return H2OAttentionManager(
         start_size=kwargs.get("start_size", 4),

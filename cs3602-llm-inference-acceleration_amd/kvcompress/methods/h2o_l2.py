@@ -9,7 +9,7 @@ import torch
 
 from .. import _engine as E
 from .. import _native as N
-from ..utils import normalize_kv_cache
+from ..utils import layer_offset, normalize_kv_cache
 
 
 def h2o_l2_compress(
@@ -21,6 +21,7 @@ def h2o_l2_compress(
     **kwargs
 ) -> List[Tuple[torch.Tensor, torch.Tensor]]:
     past_key_values = list(normalize_kv_cache(past_key_values))
+    offset = layer_offset(kwargs)  # global index of layer 0 (layer-sharded callers)
     if not past_key_values:                                           # :79
         return past_key_values
     total_cache_size = start_size + heavy_hitter_size + recent_size
@@ -29,7 +30,7 @@ def h2o_l2_compress(
         seq_len = keys.size(2)
         if seq_len <= total_cache_size:                               # :89
             continue
-        if layer_idx in skip_layers:
+        if layer_idx + offset in skip_layers:
             continue
         sink = E.py_slice(seq_len, None, start_size)[1]
         t0, tl = E.py_slice(seq_len, -recent_size)

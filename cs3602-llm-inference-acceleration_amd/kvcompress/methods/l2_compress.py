@@ -9,7 +9,7 @@ import torch
 
 from .. import _engine as E
 from .. import _native as N
-from ..utils import normalize_kv_cache
+from ..utils import layer_offset, normalize_kv_cache
 
 
 def l2_compress(
@@ -20,6 +20,7 @@ def l2_compress(
     **kwargs
 ) -> List[Tuple[torch.Tensor, torch.Tensor]]:
     past_key_values = list(normalize_kv_cache(past_key_values))
+    offset = layer_offset(kwargs)  # global index of layer 0 (layer-sharded callers)
     if keep_ratio >= 1.0:                                              # :48-49
         return past_key_values
     jobs = []
@@ -27,7 +28,7 @@ def l2_compress(
         seq_len = keys.size(2)
         if seq_len <= prune_after:                                    # :55
             continue
-        if layer_idx in skip_layers:                                  # :59
+        if layer_idx + offset in skip_layers:                         # :59
             continue
         tokens_to_keep = ceil(keep_ratio * seq_len)                   # :62
         if tokens_to_keep >= seq_len:

@@ -2,8 +2,9 @@
 
 Per-layer target sizes come from the layer's index in the list and len(list) exactly as in the
 reference.  For a layer-sharded run (one shard of a deeper stack per GPU) pass the extension
-kwargs `layer_offset` / `num_layers_total` so every shard uses the global index and depth;
-without them the behaviour is the reference's.
+kwargs `layer_offset` / `num_layers_total` so every shard uses the global index and depth (and
+`skip_layers` holds global indices, as for every method); without them the behaviour is the
+reference's.
 """
 from typing import List, Literal, Tuple
 
@@ -11,7 +12,7 @@ import torch
 
 from .. import _engine as E
 from .. import _native as N
-from ..utils import normalize_kv_cache
+from ..utils import layer_offset, normalize_kv_cache
 
 
 def pyramid_layer_sizes(num_layers, base_size=512, layer_decay=0.9, min_size=64,
@@ -43,7 +44,7 @@ def pyramid_kv_compress(
     past_key_values = list(normalize_kv_cache(past_key_values))
     if not past_key_values:
         return past_key_values
-    offset = int(kwargs.get("layer_offset", 0))
+    offset = layer_offset(kwargs)
     num_layers = int(kwargs.get("num_layers_total", len(past_key_values)))
     layer_sizes = pyramid_layer_sizes(num_layers, base_size, layer_decay, min_size, profile,
                                       offset, len(past_key_values))

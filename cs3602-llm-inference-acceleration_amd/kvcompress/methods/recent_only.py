@@ -6,7 +6,7 @@ from typing import List, Tuple
 
 import torch
 
-from ..utils import normalize_kv_cache
+from ..utils import layer_offset, normalize_kv_cache
 
 
 def recent_only_compress(
@@ -16,11 +16,12 @@ def recent_only_compress(
     **kwargs
 ) -> List[Tuple[torch.Tensor, torch.Tensor]]:
     past_key_values = list(normalize_kv_cache(past_key_values))
+    offset = layer_offset(kwargs)  # global index of layer 0 (layer-sharded callers)
     for layer_idx, (keys, values) in enumerate(past_key_values):
         seq_len = keys.size(2)
         if seq_len <= window_size:
             continue
-        if layer_idx in skip_layers:
+        if layer_idx + offset in skip_layers:
             continue
         past_key_values[layer_idx] = (keys[:, :, -window_size:, :],
                                       values[:, :, -window_size:, :])

@@ -10,7 +10,7 @@ import torch
 
 from .. import _engine as E
 from .. import _native as N
-from ..utils import normalize_kv_cache
+from ..utils import layer_offset, normalize_kv_cache
 
 
 def snapkv_lite_compress(
@@ -22,6 +22,7 @@ def snapkv_lite_compress(
     **kwargs
 ) -> List[Tuple[torch.Tensor, torch.Tensor]]:
     past_key_values = list(normalize_kv_cache(past_key_values))
+    offset = layer_offset(kwargs)  # global index of layer 0 (layer-sharded callers)
     if not past_key_values:
         return past_key_values
     jobs = []
@@ -29,7 +30,7 @@ def snapkv_lite_compress(
         seq_len = keys.size(2)
         if seq_len <= keep_size:                                      # :70
             continue
-        if layer_idx in skip_layers:
+        if layer_idx + offset in skip_layers:
             continue
         prefix_len = seq_len - observation_window                     # :83
         if prefix_len <= 0:

@@ -10,16 +10,16 @@ import torch
 
 from .. import _engine as E
 from .. import _native as N
-from ..utils import normalize_kv_cache
+from ..utils import layer_offset, normalize_kv_cache
 
 
-def _sink_recent_jobs(past_key_values, start_size, recent_size, skip_layers, fits):
+def _sink_recent_jobs(past_key_values, start_size, recent_size, skip_layers, fits, offset=0):
     jobs = []
     for layer_idx, (keys, values) in enumerate(past_key_values):
         seq_len = keys.size(2)
         if fits(seq_len):
             continue
-        if layer_idx in skip_layers:
+        if layer_idx + offset in skip_layers:
             continue
         s0, sl = E.py_slice(seq_len, None, start_size)
         t0, tl = E.py_slice(seq_len, -recent_size)
@@ -40,7 +40,7 @@ def streaming_llm_compress(
         return past_key_values
     cache_size = start_size + recent_size
     jobs = _sink_recent_jobs(past_key_values, start_size, recent_size, skip_layers,
-                             lambda S: S <= cache_size)               # :88
+                             lambda S: S <= cache_size, layer_offset(kwargs))  # :88
     E.execute(jobs, past_key_values, N.KVC_ASC, N.KVC_ALGO_SORT)
     return past_key_values
 

@@ -32,6 +32,15 @@ def normalize_kv_cache(past_key_values) -> KVList:
     return list(past_key_values)
 
 
+def layer_offset(kwargs) -> int:
+    """Global index of the first layer of the list (extension kwarg `layer_offset`, default 0).
+
+    Layer-sharded callers (one contiguous block of a deeper stack per GPU) pass
+    it so that every method tests `skip_layers` -- and pyramid_kv sizes its layers -- by GLOBAL
+    layer index, exactly as the unsharded reference call would; 0 reproduces the reference."""
+    return int(kwargs.get("layer_offset", 0))
+
+
 def _nbytes(t: torch.Tensor) -> int:
     return t.element_size() * t.nelement()
 

@@ -7,30 +7,35 @@
  *
  *     out = K[:, :, sink]  ++  K[:, :, zone][selected]  ++  K[:, :, tail]      (same for V)
  *
- * which covers every compressing branch of the eight in-scope methods:
- *   fix_size_l2   fix_size_l2.py:99-152   zone [0,S-P), select keep, tail = last P
- *   l2_compress   l2_compress.py:227-248  zone [0,S),   select ceil(kr*S)
- *   h2o_l2        h2o_l2.py:285-325       sink start, zone middle, tail recent
- *   snapkv_lite   snapkv_lite.py:88-152   zone prefix (snapkv scoring, topk), tail obs window
- *   pyramid_kv    pyramid_kv.py:300-341   sink, zone middle, tail recent (per-layer size)
- *   adaptive_l2   adaptive_l2.py:462-546  both branches
- *   streaming_llm streaming_llm.py:99-109 sink + tail, no selection (pure copy)
+ * which covers every compressing branch of the eight in-scope methods.  Each entry below names the
+ * reference lines (in /root/reference/kvcompress/methods/) whose norm -> argsort/topk -> sort ->
+ * gather -> cat sequence one call replaces:
+ *   fix_size_l2   fix_size_l2.py:99-150   zone [0,S-P), select keep, tail = last P
+ *   l2_compress   l2_compress.py:62-90    zone [0,S),   select ceil(kr*S)
+ *   h2o_l2        h2o_l2.py:99-151        sink start, zone middle, tail recent
+ *   snapkv_lite   snapkv_lite.py:83-152   zone prefix (snapkv scoring, topk), tail obs window
+ *   pyramid_kv    pyramid_kv.py:115-183   sink, zone middle, tail recent (per-layer size)
+ *   adaptive_l2   adaptive_l2.py:81-145 (hard limit), :147-199 (gradual)
+ *   streaming_llm streaming_llm.py:99-109 sink + tail, no selection (pure copy);
+ *                 evict_for_space streaming_llm.py:154-168 likewise
  * recent_only (recent_only.py:65-66) returns views and never reaches the engine.
  *
  * The reference does this with torch CPU/GPU ops (torch.norm -> argsort/topk -> sort -> gather
  * -> cat); the engine reproduces their results bit-exactly, including libstdc++'s introsort /
  * introselect tie order, torch.norm's 8-lane FMA order, and torch.gather's bf16 NaN rewrite.
  *
- * Phases (stream-ordered on `stream`, one kernel each per chunk of <= 64 layers; KVC_FUSED=1
- * runs KVC_PHASE_ALL on 128/256-byte rows as one persistent kernel instead):
+ * Phases (stream-ordered on `stream`, one kernel each per chunk of <= 64 layers; SELECT and
+ * GATHER run as one select_gather kernel unless params.flags has KVC_FLAG_SPLIT_SELECT_GATHER):
  *   SCORE  : key L2 norms of every zone token           -> workspace norm region
  *   SELECT : per (layer,b,h) row: snapkv scoring (opt.), reference-exact k-selection,
  *            ascending zone-local indices                -> workspace index region (int32)
  *   GATHER : segment copy of K and V into k_out / v_out (caller-allocated, contiguous)
  *
  * Ownership: the caller allocates outputs and the workspace; the library never allocates,
- * frees or synchronises.  Entry points are reentrant (no global mutable state) and may be used
- * concurrently on different devices/streams.  All functions return a kvc_status (0 = ok).
+ * frees or synchronises.  Entry points are reentrant (no global mutable state, no environment
+ * variables read) and may be used concurrently on different devices/streams.  All functions
+ * return a kvc_status (0 = ok); a HIP launch failure is reported from that launch's own return
+ * value, and a caller's pending HIP error is left untouched.
  */
 #ifndef KVC_H
 #define KVC_H
@@ -42,7 +47,7 @@
 extern "C" {
 #endif
 
-#define KVC_ABI_VERSION 1
+#define KVC_ABI_VERSION 2
 
 typedef struct ihipStream_t* kvc_stream_t; /* a hipStream_t; NULL = legacy default stream */
 
@@ -63,6 +68,9 @@ enum kvc_phase {
   KVC_PHASE_SELECT = 2,
   KVC_PHASE_GATHER = 4,
   KVC_PHASE_ALL = 7
+};
+enum kvc_flag {
+  KVC_FLAG_SPLIT_SELECT_GATHER = 1 /* SELECT writes the index region, then a GATHER kernel */
 };
 enum kvc_status {
   KVC_OK = 0,
@@ -110,11 +118,11 @@ typedef struct kvc_params {
   int32_t algo;           /* enum kvc_algo  */
   int32_t phases;         /* OR of enum kvc_phase */
   int32_t external_index; /* 1: GATHER reads indices the caller wrote into the index region */
+  int32_t flags;          /* OR of enum kvc_flag */
+  int32_t reserved;       /* 0 */
 } kvc_params_t;
 
 typedef struct kvc_plan_info {
-  size_t control_offset;   /* workspace byte offset of the fused kernel's control words   */
-  size_t desc_offset;      /* workspace byte offset of the device copy of the layer table */
   size_t norm_offset;      /* workspace byte offset of the norm region                    */
   size_t index_offset;     /* workspace byte offset of the int32 index region             */
   size_t workspace_bytes;  /* total workspace the launch needs                              */
@@ -136,16 +144,12 @@ const char* kvc_status_string(int status);
 int kvc_plan(const kvc_params_t* params, kvc_layer_t* layers, int num_layers,
              kvc_plan_info_t* info);
 
-/* Launches the requested phases.  `layers` is the host table filled by kvc_plan(); the score /
- * select / gather kernels receive it by value in their kernel arguments (no copy is enqueued).
- * `layers_dev` is only used by the opt-in fused kernel (KVC_FUSED=1): a device copy of the table
- * (e.g. at workspace + info.desc_offset) already stream-ordered with this launch, or NULL to let
- * the library enqueue that copy itself.  Pass NULL. */
-int kvc_launch(const kvc_params_t* params, const kvc_layer_t* layers,
-               const kvc_layer_t* layers_dev, int num_layers, void* workspace,
-               size_t workspace_bytes, kvc_stream_t stream);
+/* Launches the requested phases.  `layers` is the host table filled by kvc_plan(); the kernels
+ * receive it by value in their kernel arguments (no copy is enqueued). */
+int kvc_launch(const kvc_params_t* params, const kvc_layer_t* layers, int num_layers,
+               void* workspace, size_t workspace_bytes, kvc_stream_t stream);
 
-/* Convenience: kvc_plan + kvc_launch(layers_dev = NULL).  `layers` is updated in place. */
+/* Convenience: kvc_plan + kvc_launch.  `layers` is updated in place. */
 int kvc_compress(const kvc_params_t* params, kvc_layer_t* layers, int num_layers,
                  void* workspace, size_t workspace_bytes, kvc_stream_t stream);
 

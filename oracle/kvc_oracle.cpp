@@ -9,7 +9,7 @@
 //
 // What is restated (reference call sites in brackets):
 //   * torch.norm(x, p=2, dim=-1)                               [methods/fix_size_l2.py:106,
-//     l2_compress.py:228, h2o_l2.py:296, snapkv_lite.py:96, pyramid_kv.py:313, adaptive_l2.py:473,527]
+//     l2_compress.py:70, h2o_l2.py:122, snapkv_lite.py:96, pyramid_kv.py:155, adaptive_l2.py:126,180]
 //     fp32/bf16 rows (aten's vectorised reduce-lastdim norm_two_reduce_step)
 //     = 8 fp32 lane accumulators, lane j: acc_j = fma(x[d], x[d], acc_j) for d = j, j+8, ...;
 //       serial lane sum ((a0+a1)+a2)+...+a7; correctly rounded fp32 sqrt; RNE to the storage dtype.

@@ -164,7 +164,7 @@ def l2_compress(layers, keep_ratio=1.0, prune_after=1000, skip_layers=(0, 1), **
         if k >= S:
             continue
         if k < -1:
-            raise RuntimeError("expand with negative size (reference l2_compress.py:240)")
+            raise RuntimeError("expand with negative size (reference l2_compress.py:82)")
         order = argsort_prefix(norms(keys), S)[:, :, :k]
         idx = np.sort(order, axis=-1)
         out[i] = (np.ascontiguousarray(gather(keys, idx)),
@@ -215,6 +215,27 @@ def streaming_llm_compress(layers, start_size=4, recent_size=508, skip_layers=()
             continue
         out[i] = (cat([keys[:, :, :start_size], keys[:, :, -recent_size:]]),
                   cat([values[:, :, :start_size], values[:, :, -recent_size:]]), "new")
+    return out
+
+
+def evict_for_space(layers, num_coming, start_size=4, recent_size=508, skip_layers=()):
+    """streaming_llm.py:114-170 (exported, not registered): the length test includes the
+    incoming tokens, and the recent window shrinks by them unless that empties it."""
+    out = [(k, v, "same") for k, v in layers]
+    if not layers:
+        return out
+    cache_size = start_size + recent_size
+    for i, (keys, values) in enumerate(layers):
+        S = keys.shape[2]
+        if S + num_coming <= cache_size:                               # :149
+            continue
+        if i in skip_layers:                                           # :152
+            continue
+        eff = recent_size - num_coming                                 # :156-158
+        if eff <= 0:
+            eff = recent_size
+        out[i] = (cat([keys[:, :, :start_size], keys[:, :, -eff:]]),
+                  cat([values[:, :, :start_size], values[:, :, -eff:]]), "new")
     return out
 
 
@@ -389,4 +410,5 @@ METHODS = {
     "snapkv_lite": snapkv_lite_compress,
     "pyramid_kv": pyramid_kv_compress,
     "adaptive_l2": adaptive_l2_compress,
+    "evict_for_space": evict_for_space,  # not in the reference's registry; goldens only
 }

@@ -1,7 +1,11 @@
 """Generate golden fixtures by running the UNMODIFIED reference kvcompress (build container only).
 
     cd /root/repo && PYTHONPATH=/root/reference PYTHONDONTWRITEBYTECODE=1 \
-        python tests/golden/gen_goldens.py [--prims-only]
+        python tests/golden/gen_goldens.py [--prims-only | --append]
+
+--append runs only the cases added after the last generation (ids are positional, so new cases
+are only ever appended) and merges them into cases.json / positions.npz; the earlier cases'
+definitions must be unchanged (checked).
 
 The reference is imported from /root/reference (read-only); nothing of it is copied.  Outputs
 (data only) go to tests/golden/:
@@ -30,6 +34,7 @@ assert os.path.abspath(os.environ.get("PYTHONPATH", "").split(":")[0]) == "/root
     "run with PYTHONPATH=/root/reference"
 import kvcompress  # noqa: E402  (the reference)
 from kvcompress.methods import get_compress_fn, list_methods  # noqa: E402
+from kvcompress.methods.streaming_llm import evict_for_space  # noqa: E402  (exported, unregistered)
 
 torch.set_num_threads(8)
 
@@ -233,10 +238,41 @@ def build_cases():
             add("h2o_l2", {"start_size": 4, "heavy_hitter_size": 64, "recent_size": 444}, dt,
                 [L((1, 4, 2048, D), s + 195 + D), L((1, 4, 513, D), s + 196 + D, "scaled")],
                 f"D{D}")
+    # ---- round 2: the BASELINE configs at their exact geometries (pythia-2.8b: D = 80,
+    # pythia-6.9b: D = 128, 32 heads), and evict_for_space (streaming_llm.py:114-170) ----
+    add("fix_size_l2", {"fix_kv_size": 512, "keep_ratio": 0.0, "strategy": "keep_low",
+                        "skip_layers": []}, "bf16", [L((1, 32, 4096, 80), s + 300)], "cfg2_D80")
+    add("h2o_l2", {"start_size": 4, "heavy_hitter_size": 64, "recent_size": 444}, "bf16",
+        [L((1, 32, 16384, 80), s + 301)], "cfg4_S16384_D80")
+    add("streaming_llm", {"start_size": 4, "recent_size": 1020}, "bf16",
+        [L((1, 32, 16384, 80), s + 302)], "cfg3_S16384_D80")
+    add("snapkv_lite", {"observation_window": 32, "keep_size": 512, "pooling_kernel": 5}, "bf16",
+        [L((1, 32, 16384, 128), s + 303)], "cfg5_S16384_pk5")
+    # pyramid_kv over a whole 32-layer pythia-6.9b stack: layers >= 20 hit the min_size clamp
+    add("pyramid_kv", {"base_size": 512}, "bf16",
+        [L((1, 32, 1500, 128), s + 310 + j) for j in range(32)], "cfg5_32layers")
+    for dt in ("bf16", "fp16", "fp32"):
+        add("evict_for_space", {"num_coming": 1, "start_size": 4, "recent_size": 508}, dt,
+            [L((1, 4, 512, 64), s + 350), L((1, 4, 511, 64), s + 351),
+             L((1, 4, 1000, 80), s + 352)], "one")
+    add("evict_for_space", {"num_coming": 600, "start_size": 4, "recent_size": 508}, "bf16",
+        [L((1, 2, 100, 64), s + 353), L((1, 2, 2000, 64), s + 354)], "coming_gt_recent")
+    add("evict_for_space", {"num_coming": 508, "start_size": 4, "recent_size": 508,
+                            "skip_layers": [1]}, "bf16",
+        [L((1, 2, 700, 64), s + 355), L((1, 2, 700, 64), s + 356), L((1, 2, 3, 64), s + 357)],
+        "coming_eq_recent_skip")
+    add("evict_for_space", {"num_coming": 0, "start_size": 4, "recent_size": 0}, "bf16",
+        [L((1, 2, 30, 64), s + 358)], "recent0_quirk")
+    add("evict_for_space", {"num_coming": 100, "start_size": 0, "recent_size": 1020}, "bf16",
+        [L((1, 32, 16384, 80), s + 359)], "S16384_D80")
+
+
+def method_fn(name):
+    return evict_for_space if name == "evict_for_space" else get_compress_fn(name)
 
 
 def run_case(case, positions):
-    fn = get_compress_fn(case["method"])
+    fn = method_fn(case["method"])
     dt = case["dtype"]
     rec = dict(case)
     layers = make_layers(case)
@@ -330,7 +366,30 @@ def write_prims(meta):
     return pm, sm
 
 
+def append_new():
+    with open(os.path.join(HERE, "cases.json")) as f:
+        old = json.load(f)
+    have = old["cases"]
+    build_cases()
+    for rec, c in zip(have, CASES):  # earlier definitions must be untouched
+        assert rec["id"] == c["id"] and rec["kwargs"] == c["kwargs"] and \
+            rec["layers"] == c["layers"], rec["id"]
+    positions = dict(np.load(os.path.join(HERE, "positions.npz")))
+    new = []
+    for c in CASES[len(have):]:
+        new.append(run_case(c, positions))
+        print(c["id"], "error" if new[-1]["error"] else "ok", flush=True)
+    old["cases"] = have + new
+    with open(os.path.join(HERE, "cases.json"), "w") as f:
+        json.dump(old, f, indent=1)
+    np.savez_compressed(os.path.join(HERE, "positions.npz"), **positions)
+    print("appended", len(new), "cases; total", len(old["cases"]))
+
+
 def main():
+    if "--append" in sys.argv:
+        append_new()
+        return
     if "--prims-only" in sys.argv:
         with open(os.path.join(HERE, "cases.json")) as f:
             meta = json.load(f)["meta"]

@@ -29,9 +29,9 @@ def test_library_exports_every_declared_symbol():
 def test_struct_layout():
     L = N.lib()
     assert L.kvc_layer_struct_size() == N.LAYER_DTYPE.itemsize == 136
-    assert ctypes.sizeof(N.Params) == 32
-    assert ctypes.sizeof(N.PlanInfo) == 80
-    assert L.kvc_version() == 1
+    assert ctypes.sizeof(N.Params) == 40
+    assert ctypes.sizeof(N.PlanInfo) == 64
+    assert L.kvc_version() == N.ABI_VERSION == 2
     assert L.kvc_max_zone_len() == 1 << 24
 
 
@@ -63,7 +63,7 @@ def test_plan_fills_prefix_fields_and_layout():
     assert list(table["unit0"]) == [0, 2 * 32 * 512 * 16, 4 * 32 * 512 * 16]
     assert info.gather_units == 2 * 32 * 16 * (512 + 512 + 1024)
     assert info.rows == 96 and info.norm_row_stride == 16384 and info.index_row_stride == 512
-    assert info.norm_offset >= 3 * 136 and info.index_offset >= info.norm_offset + 96 * 16384 * 2
+    assert info.norm_offset == 0 and info.index_offset >= info.norm_offset + 96 * 16384 * 2
 
 
 @pytest.mark.parametrize("bad, code", [
@@ -152,4 +152,4 @@ def test_launch_revalidates_against_plan():
     rc, info = N.plan(_params(), table)
     assert rc == 0
     table["unit0"] = 7  # tampered plan fields are rejected before any HIP call
-    assert N.launch(_params(), table, 0, 0, 0, 0) == -1
+    assert N.launch(_params(), table, 0, 0, 0) == -1

@@ -1,0 +1,80 @@
+"""bench.py's multi-GPU launch contract, checked on CPU with its --dry-run harness (gloo, a
+stand-in step whose last rank is the slow one, no engine and no GPU):
+  * `python bench.py --gpus 2` starts two ranks itself and prints ONE JSON line, n_gpus = 2;
+  * under torchrun (WORLD_SIZE set) it spawns nothing and reports the same way;
+  * the reported time is the MAX over ranks (the slow rank's).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STEPS = 5
+
+
+def _json_lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+def _check(lines, n):
+    assert len(lines) == 1, lines
+    r = lines[0]
+    assert r["n_gpus"] == n and r["steps"] == STEPS and r["dry_run"] is True
+    assert r["config"]["layers_total"] == 32 * n  # weak scaling: 32 layers per rank
+    # the last rank sleeps 2 ms * n per step: the max over ranks is at least that
+    assert r["ms_per_step"] >= 2.0 * n * 0.95, r["ms_per_step"]
+    assert r["value"] > 0
+
+
+def _free_port():
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    return port
+
+
+def _env():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def test_gpus_flag_spawns_ranks():
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--gpus",
+                          "2", "--steps", str(STEPS), "--warmup", "2"], cwd=ROOT, env=_env(),
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    _check(_json_lines(out.stdout), 2)
+
+
+def test_torchrun_launch_does_not_respawn():
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                          str(_free_port()), os.path.join(ROOT, "bench.py"), "--dry-run", "--gpus", "2",
+                          "--steps", str(STEPS), "--warmup", "2"], cwd=ROOT, env=_env(),
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    _check(_json_lines(out.stdout), 2)
+
+
+def test_single_rank_default():
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--steps",
+                          str(STEPS), "--warmup", "1"], cwd=ROOT, env=_env(),
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    _check(_json_lines(out.stdout), 1)
+
+
+def test_strong_scaling_workload_splits_32_layers():
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--gpus",
+                          "2", "--workload", "cfg4-h2o-l32", "--steps", str(STEPS), "--warmup",
+                          "1"], cwd=ROOT, env=_env(), capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r, = _json_lines(out.stdout)
+    assert r["scaling"] == "strong" and r["config"]["layers_total"] == 32
+    assert r["config"]["layers_per_gpu"] == 16

@@ -1,0 +1,52 @@
+"""Every `file.py:N[-M]` citation of a reference file in this repo lands inside that file.
+
+Citations are how a reader checks parity against /root/reference, so a line range past the end
+of the cited file is a defect.  Runs where the reference is mounted (the build container); the
+GPU box has no /root/reference and skips it.
+"""
+import os
+import re
+
+import pytest
+
+REF = "/root/reference"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SKIP_DOCS = {"VERDICT.md", "ADVICE.md", "SURVEY.md", "BASELINE.md"}  # not authored here
+PAT = re.compile(r"((?:[A-Za-z_][\w.-]*/)*[A-Za-z_][\w-]*\.py):(\d+)(?:-(\d+))?")
+
+
+def _reference_files():
+    out = {}
+    for root, _, fs in os.walk(REF):
+        for f in fs:
+            if f.endswith(".py"):
+                p = os.path.join(root, f)
+                out[os.path.relpath(p, REF)] = sum(1 for _ in open(p, errors="ignore"))
+    return out
+
+
+def _resolve(cited, ref):
+    """Line counts of the reference files a (possibly partial) path can name."""
+    return [n for rel, n in ref.items() if rel == cited or rel.endswith("/" + cited)]
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference not mounted")
+def test_reference_citations_in_range():
+    ref = _reference_files()
+    bad = []
+    for root, dirs, fs in os.walk(ROOT):
+        dirs[:] = [d for d in dirs if d not in (".git", "golden", "gpurun_out", "profiles")]
+        for f in fs:
+            if not f.endswith((".py", ".h", ".hip", ".cpp", ".md")) or f in SKIP_DOCS:
+                continue
+            p = os.path.join(root, f)
+            for ln, line in enumerate(open(p, errors="ignore"), 1):
+                for m in PAT.finditer(line):
+                    counts = _resolve(m.group(1), ref)
+                    if not counts:
+                        continue  # one of this repo's own files
+                    hi = int(m.group(3) or m.group(2))
+                    if hi > max(counts):
+                        bad.append(f"{os.path.relpath(p, ROOT)}:{ln}: {m.group(0)} "
+                                   f"(file has {max(counts)} lines)")
+    assert not bad, "\n".join(bad)

@@ -44,6 +44,20 @@ def _layers(n, S=1000):
             for i in range(n)]
 
 
+# every registered method with a layer-sharding-sensitive configuration: skip_layers (global ids,
+# the reference's defaults where it has them) and, for pyramid_kv, the depth-dependent sizes
+SHARD_CASES = (
+    ("pyramid_kv", dict(base_size=512, layer_decay=0.8, skip_layers=[3]), True),
+    ("fix_size_l2", dict(fix_kv_size=256, keep_ratio=0.5), False),        # default skip [0, 1]
+    ("l2_compress", dict(keep_ratio=0.8, prune_after=100), False),         # default skip [0, 1]
+    ("h2o_l2", dict(start_size=4, heavy_hitter_size=64, recent_size=444, skip_layers=[5]), False),
+    ("snapkv_lite", dict(observation_window=32, keep_size=512, skip_layers=[0, 9]), False),
+    ("adaptive_l2", dict(target_size=256, skip_layers=[2, 7]), False),
+    ("streaming_llm", dict(start_size=4, recent_size=300, skip_layers=[4]), False),
+    ("recent_only", dict(window_size=512), False),                        # default skip [0, 1]
+)
+
+
 def _worker_shard(rank, world, port, q):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "cs3602-llm-inference-acceleration_amd"))
@@ -51,25 +65,28 @@ def _worker_shard(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from bench import shard_layers
-    from kvcompress.methods import pyramid_kv_compress, fix_size_l2_compress
+    from kvcompress.methods import get_compress_fn
     L = 10
     allL = _layers(L)
     a, b = shard_layers(L, world, rank)
     mine = allL[a:b]
     plans = {}
-    for name, fn, kw in (("pyramid", pyramid_kv_compress,
-                          dict(base_size=512, layer_decay=0.8, skip_layers=[3],
-                               layer_offset=a, num_layers_total=L)),
-                         ("fix", fix_size_l2_compress, dict(fix_kv_size=256, keep_ratio=0.5))):
-        rec, _ = _capture_plans(fn, list(mine), **kw)
-        plans[name] = [(r[0] + a,) + r[1:] for r in rec]  # to global layer ids
+    for name, kw, depth in SHARD_CASES:
+        extra = dict(layer_offset=a, num_layers_total=L) if depth else dict(layer_offset=a)
+        rec, out = _capture_plans(get_compress_fn(name), list(mine), **kw, **extra)
+        shapes = [(a + i, tuple(k.shape)) for i, (k, _) in enumerate(out)]
+        plans[name] = ([(r[0] + a,) + r[1:] for r in rec], shapes)  # to global layer ids
     gathered = [None] * world
     dist.all_gather_object(gathered, plans)
     if rank == 0:
-        merged = {k: sorted(sum((g[k] for g in gathered), [])) for k in plans}
-        ref_p, _ = _capture_plans(pyramid_kv_compress, list(allL), base_size=512,
-                                  layer_decay=0.8, skip_layers=[3])
-        q.put((merged["pyramid"] == sorted(ref_p), merged["pyramid"], sorted(ref_p)))
+        res = {}
+        for name, kw, _ in SHARD_CASES:
+            got = (sorted(sum((g[name][0] for g in gathered), [])),
+                   sorted(sum((g[name][1] for g in gathered), [])))
+            ref, out = _capture_plans(get_compress_fn(name), list(allL), **kw)
+            want = (sorted(ref), sorted((i, tuple(k.shape)) for i, (k, _) in enumerate(out)))
+            res[name] = (got == want, got, want)
+        q.put(res)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -105,8 +122,13 @@ def _run(worker, world=2):
 
 
 def test_sharded_plans_equal_unsharded():
-    (ok, got, ref), = _run(_worker_shard)
-    assert ok, (got, ref)
+    """Every method, sharded over 2 ranks with layer_offset, plans exactly the engine jobs (and
+    returns the layer shapes) of the unsharded reference call."""
+    res, = _run(_worker_shard)
+    assert set(res) == {c[0] for c in SHARD_CASES}
+    for name, (ok, got, want) in res.items():
+        assert ok, (name, got, want)
+        assert got[0] or name == "recent_only", name  # the case exercises the engine
 
 
 def test_timing_is_max_over_ranks():

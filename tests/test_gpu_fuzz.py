@@ -43,9 +43,9 @@ def _kwargs(rng, method, S):
 @pytest.mark.parametrize("case", range(N_CASES))
 def test_random_configs_match_oracle(case, monkeypatch):
     from kvcompress.methods import get_compress_fn
-    # launch paths in rotation: SCORE + SELECT_GATHER, three kernels, the fused persistent kernel
-    monkeypatch.setenv("KVC_SEL_GATHER", "0" if case % 3 == 1 else "1")
-    monkeypatch.setenv("KVC_FUSED", "1" if case % 3 == 2 else "0")
+    # launch paths in rotation: SCORE + SELECT_GATHER, and SCORE / SELECT / GATHER
+    from kvcompress import _engine
+    monkeypatch.setattr(_engine, "split_select_gather", case % 2 == 1)
     rng = np.random.default_rng(90000 + case)
     method = str(rng.choice(["fix_size_l2", "l2_compress", "streaming_llm", "h2o_l2",
                              "snapkv_lite", "pyramid_kv", "adaptive_l2", "recent_only"]))

@@ -15,6 +15,9 @@ pytestmark = pytest.mark.gpu
 
 def _method(name):
     from kvcompress.methods import get_compress_fn
+    if name == "evict_for_space":  # exported by streaming_llm, not in the registry
+        from kvcompress.methods.streaming_llm import evict_for_space
+        return evict_for_space
     return get_compress_fn(name)
 
 
@@ -26,13 +29,12 @@ def _run_case(case, values):
     return tin, out
 
 
-@pytest.fixture(params=["kernels", "separate", "fused"])
+@pytest.fixture(params=["kernels", "separate"])
 def launch_path(request, monkeypatch):
-    """Every launch path of kvc_launch: the default SCORE + SELECT_GATHER kernels ("kernels"),
-    SCORE / SELECT / GATHER as three kernels (KVC_SEL_GATHER=0, "separate"), and the opt-in
-    fused persistent kernel (KVC_FUSED=1, 128/256-byte rows)."""
-    monkeypatch.setenv("KVC_FUSED", "1" if request.param == "fused" else "0")
-    monkeypatch.setenv("KVC_SEL_GATHER", "0" if request.param == "separate" else "1")
+    """Both launch paths of kvc_launch: the default SCORE + SELECT_GATHER kernels ("kernels") and
+    SCORE / SELECT / GATHER as three kernels (KVC_FLAG_SPLIT_SELECT_GATHER, "separate")."""
+    from kvcompress import _engine
+    monkeypatch.setattr(_engine, "split_select_gather", request.param == "separate")
     return request.param
 
 
@@ -86,7 +88,7 @@ def _abi_select(keys_np, n_select, order, algo, score_mode=0, pool=0, zone=None)
     rc, info = N.plan(p, table)
     assert rc == 0
     ws = torch.zeros(int(info.workspace_bytes), dtype=torch.uint8, device=K.device)
-    rc = N.launch(p, table, 0, ws.data_ptr(), int(info.workspace_bytes),
+    rc = N.launch(p, table, ws.data_ptr(), int(info.workspace_bytes),
                   torch.cuda.current_stream().cuda_stream)
     assert rc == 0
     torch.cuda.synchronize()
@@ -283,3 +285,41 @@ def test_zones_beyond_u16_positions(dtype):
             for li, ((ko, vo), (rk, rv, _)) in enumerate(zip(out, refs)):
                 assert np.array_equal(to_np(ko), rk), (S, fn.__name__, kw, li)
                 assert np.array_equal(to_np(vo), rv), (S, fn.__name__, kw, li)
+
+
+SHARDED = (
+    ("pyramid_kv", dict(base_size=512, layer_decay=0.9, skip_layers=[9])),
+    ("fix_size_l2", dict(fix_kv_size=256, keep_ratio=0.5)),            # default skip [0, 1]
+    ("h2o_l2", dict(start_size=4, heavy_hitter_size=64, recent_size=444, skip_layers=[17])),
+    ("snapkv_lite", dict(observation_window=32, keep_size=512, skip_layers=[30])),
+    ("adaptive_l2", dict(target_size=512, skip_layers=[8, 24])),
+    ("l2_compress", dict(keep_ratio=0.8, prune_after=100)),            # default skip [0, 1]
+    ("streaming_llm", dict(start_size=4, recent_size=500, skip_layers=[31])),
+)
+
+
+@pytest.mark.parametrize("name,kw", SHARDED, ids=[s[0] for s in SHARDED])
+def test_layer_sharded_calls_match_unsharded_oracle(name, kw):
+    """a 32-layer stack split into 4 contiguous shards (the 8-GPU layout with 8
+    layers per shard, here on one device), each compressed by its own call with the extension
+    kwargs layer_offset (global skip_layers) / num_layers_total (pyramid_kv's depth-dependent
+    sizes, pyramid_kv.py:82-97: layers >= 20 at min_size), is bit-identical to the unsharded
+    reference call (the oracle) on the whole stack."""
+    from bench import shard_layers
+    dt = "bf16"
+    L, shape = 32, (1, 8, 1200, 64)
+    layers = [(prng.gen_keys(4000 + i, shape, dt, "normal"), prng.gen_values(4000 + i, shape, dt))
+              for i in range(L)]
+    ref = oracle.METHODS[name](layers, **kw)
+    fn = _method(name)
+    got = []
+    for r in range(4):
+        a, b = shard_layers(L, 4, r)
+        extra = dict(layer_offset=a)
+        if name == "pyramid_kv":
+            extra["num_layers_total"] = L
+        got += fn([(to_dev(k), to_dev(v)) for k, v in layers[a:b]], **kw, **extra)
+    torch.cuda.synchronize()
+    assert len(got) == L
+    for li, ((ko, vo), (rk, rv, _)) in enumerate(zip(got, ref)):
+        assert np.array_equal(to_np(ko), rk) and np.array_equal(to_np(vo), rv), (name, li)

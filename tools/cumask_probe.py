@@ -59,7 +59,7 @@ def make(layers):
 def run(tab, phases, stream):
     p, t, info, ws = tab
     p.phases = phases
-    rc = N.launch(p, t, 0, ws.data_ptr(), int(info.workspace_bytes), stream.cuda_stream)
+    rc = N.launch(p, t, ws.data_ptr(), int(info.workspace_bytes), stream.cuda_stream)
     assert rc == 0
 
 

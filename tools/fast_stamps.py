@@ -18,7 +18,7 @@ for i, K in enumerate(Ks):
 p = N.Params(dtype=N.KVC_F32, batch=1, heads=H, head_dim=D, order=0, algo=0, phases=N.PHASE_SCORE | N.PHASE_SELECT, external_index=0)
 rc, info = N.plan(p, table); assert rc == 0
 ws = torch.zeros(int(info.workspace_bytes), dtype=torch.uint8, device=dev)
-rc = N.launch(p, table, 0, ws.data_ptr(), int(info.workspace_bytes), torch.cuda.current_stream().cuda_stream); assert rc == 0
+rc = N.launch(p, table, ws.data_ptr(), int(info.workspace_bytes), torch.cuda.current_stream().cuda_stream); assert rc == 0
 torch.cuda.synchronize()
 rows = int(info.rows)
 st = ws[-rows * 256:].view(torch.int64).view(rows, 32).cpu().numpy().astype(np.float64)

@@ -20,14 +20,10 @@ if [ "$MODE" = "all" ] || [ "$MODE" = "bench" ]; then
       -- python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline > "$R/gpurun_out/prof.log" 2>&1 || exit $?
   find "$R/gpurun_out/prof" -name "*stats*" | head
 fi
-if [ "$MODE" = "micro" ]; then
-  timeout -k 10 300 python tools/microbench.py "${2:-lds,direct}" "${3:-5}" > gpurun_out/micro.json 2> gpurun_out/micro.err || exit $?
-  cat gpurun_out/micro.json
-fi
 if [ "$MODE" = "stamps" ]; then
   : > gpurun_out/stamps.json
-  for ws in ${2:-1024}; do
-    KVC_WAVE_SEG=$ws timeout -k 10 300 python tools/select_stamps.py >> gpurun_out/stamps.json 2>> gpurun_out/stamps.err || exit $?
+  for ws in 1; do
+    timeout -k 10 300 python tools/select_stamps.py >> gpurun_out/stamps.json 2>> gpurun_out/stamps.err || exit $?
   done
   cat gpurun_out/stamps.json
 fi

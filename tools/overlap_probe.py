@@ -43,11 +43,10 @@ B = make(range(16, 32))
 def run(tab, phases, stream):
     p, t, info, ws = tab
     p.phases = phases
-    rc = N.launch(p, t, 0, ws.data_ptr(), int(info.workspace_bytes), stream.cuda_stream)
+    rc = N.launch(p, t, ws.data_ptr(), int(info.workspace_bytes), stream.cuda_stream)
     assert rc == 0
 
 
-os.environ["KVC_FUSED"] = "0"
 SEL = N.PHASE_SELECT if os.environ.get("OVERLAP_PHASES") == "select" else (N.PHASE_SELECT | N.PHASE_GATHER)
 s1 = torch.cuda.Stream(device=dev)
 s2 = torch.cuda.Stream(device=dev, priority=-1 if os.environ.get("OVERLAP_PRIO", "1") == "1" else 0)

@@ -21,7 +21,7 @@ layers = [(torch.randn(1, 32, S, 128, device=dev, generator=g).to(dt),
            torch.randn(1, 32, S, 128, device=dev, generator=g).to(dt)) for _ in range(32)]
 res = {"lib": os.path.basename(os.environ.get("KVC_LIB", "libkvc.so")), "dtype": str(dt)}
 for name, steps in (("three", _engine.PhaseTimer.THREE), ("two", _engine.PhaseTimer.DEFAULT)):
-    os.environ["KVC_SEL_GATHER"] = "0" if name == "three" else "1"
+    _engine.split_select_gather = name == "three"
     for _ in range(3):
         fix_size_l2_compress(layers, fix_kv_size=512, skip_layers=[])
     t = _engine.PhaseTimer(steps=steps)

@@ -33,9 +33,9 @@ p = N.Params(dtype=N.KVC_BF16, batch=1, heads=H, head_dim=D, order=0, algo=0,
 rc, info = N.plan(p, table)
 assert rc == 0
 ws = torch.zeros(int(info.workspace_bytes), dtype=torch.uint8, device=dev)
-res = {"wave_seg": os.environ.get("KVC_WAVE_SEG", "default")}
+res = {"wave_seg": "compile-time kWaveSeg"}
 for rep in range(3):
-    rc = N.launch(p, table, 0, ws.data_ptr(), int(info.workspace_bytes),
+    rc = N.launch(p, table, ws.data_ptr(), int(info.workspace_bytes),
                   torch.cuda.current_stream().cuda_stream)
     assert rc == 0
     torch.cuda.synchronize()
