@@ -21,7 +21,7 @@ def py_slice(S, start=None, stop=None):
     return r.start, len(r)
 
 
-@dataclass
+@dataclass(slots=True)
 class Segments:
     """out = X[:, :, 0:sink_len] ++ X[:, :, zone][selected] ++ X[:, :, tail]  (X = K and V)."""
     layer_idx: int
@@ -112,12 +112,45 @@ def _prep(t):
 def execute(jobs: List[Segments], out_list: list, order: int, algo: int):
     if not jobs:
         return
+    fast = _one_plain_group(jobs)
+    if fast is not None:
+        _run_plain(*fast, jobs, out_list, order, algo)
+        return
     groups = {}
     for j in jobs:
         B, H, _, D = _check_tensors(j)
         groups.setdefault((j.keys.get_device(), j.keys.dtype, B, H, D), []).append(j)
     for (device, dtype, B, H, D), js in groups.items():
         _run_group(device, dtype, B, H, D, js, out_list, order, algo)
+
+
+def _one_plain_group(jobs):
+    """The common call in ONE pass over its layers: every layer's K/V on one ROCm device, one
+    supported dtype, one (B, H, D), plain contiguous, engine-selected.  Returns the group key,
+    the K/V data pointers and the per-layer (S, segment bounds) -- or None for anything else
+    (the general path then checks and groups every layer)."""
+    k0 = jobs[0].keys
+    dt, shape0 = k0.dtype, k0.shape
+    if dt not in _SUPPORTED or len(shape0) != 4 or not k0.is_cuda:
+        return None
+    B, H, _, D = shape0
+    if (D * _ESIZE[dt]) % 16:
+        return None
+    dev = k0.get_device()
+    kps, vps, segs = [], [], []
+    for j in jobs:
+        k, v = j.keys, j.values
+        ks = k.shape
+        if (j.ext_index is not None or k.dtype is not dt or v.dtype is not dt or
+                v.shape != ks or len(ks) != 4 or ks[0] != B or ks[1] != H or ks[3] != D or
+                not (k.is_contiguous() and v.is_contiguous()) or k.get_device() != dev or
+                v.get_device() != dev):
+            return None
+        kps.append(k.data_ptr())
+        vps.append(v.data_ptr())
+        segs.append((ks[2], j.zone_start, j.zone_len, j.n_select, j.sink_len, j.tail_start,
+                     j.tail_len, j.pool_kernel, j.score_mode))
+    return dev, dt, B, H, D, kps, vps, segs
 
 
 def _upload(params, table, device, js, B, H):
@@ -157,28 +190,132 @@ def _launch(params, table, ws, info, stream, phases):
     params.phases = saved
 
 
+class _PlanCache:
+    """Plans of recent call shapes, so that a repeated call (the per-token decode step: same
+    layer count, shapes and segment bounds every step) skips kvc_plan, the layer-table build and
+    the workspace allocation and only writes the four pointer columns of its table.
+
+    Key: (device, stream, dtype, B, H, D, order, algo, split flag, per-layer (S, segments)) of a
+    group whose K/V are plain contiguous tensors.  Value: the planned table (pointer columns
+    zero), kvc_plan_info, the workspace and the params.  A workspace is reused only by calls on
+    the SAME stream, which are ordered behind the kernels that used it before.  Calls with
+    caller-provided indices (strategy="random") are not cached: their workspace holds per-call
+    data."""
+
+    def __init__(self, capacity=8):
+        self.capacity = capacity
+        self.entries = {}
+
+    def get(self, key):
+        e = self.entries.get(key)
+        if e is not None and len(self.entries) > 1:  # most recently used last
+            del self.entries[key]
+            self.entries[key] = e
+        return e
+
+    def put(self, key, entry):
+        if len(self.entries) >= self.capacity:
+            del self.entries[next(iter(self.entries))]
+        self.entries[key] = entry
+
+    def clear(self):
+        self.entries.clear()
+
+
+plan_cache = _PlanCache()
+
+
+def _params(dtype, B, H, D, order, algo, external):
+    return N.Params(dtype=_SUPPORTED[dtype], batch=B, heads=H, head_dim=D, order=order,
+                    algo=algo, phases=N.PHASE_GATHER if external else N.PHASE_ALL,
+                    external_index=1 if external else 0,
+                    flags=N.FLAG_SPLIT_SELECT_GATHER if split_select_gather else 0)
+
+
+def _outputs(device, dtype, B, H, D, n_outs):
+    """Fresh contiguous [B,H,n_out,D] K and V per layer, and their data pointers.  Layers of one
+    output length share one allocation (decode steps: 64 tensors per token); each layer's K / V
+    is a disjoint contiguous view of it ("Output tensors")."""
+    n = len(n_outs)
+    if all(x == n_outs[0] for x in n_outs):
+        buf = torch.empty((2 * n, B, H, n_outs[0], D), dtype=dtype, device=device)
+        o = buf.unbind(0)
+        step = B * H * n_outs[0] * D * _ESIZE[dtype]
+        offs = np.arange(2 * n, dtype=np.uint64) * np.uint64(step) + np.uint64(buf.data_ptr())
+        return o[:n], o[n:], offs[:n], offs[n:]
+    kos = [torch.empty((B, H, x, D), dtype=dtype, device=device) for x in n_outs]
+    vos = [torch.empty((B, H, x, D), dtype=dtype, device=device) for x in n_outs]
+    return kos, vos, [t.data_ptr() for t in kos], [t.data_ptr() for t in vos]
+
+
+def _run_plain(device, dtype, B, H, D, kps, vps, segs, js, out_list, order, algo):
+    """One launch for a plain group (see _one_plain_group), its plan taken from plan_cache."""
+    with torch.cuda.device(device):
+        stream = torch.cuda.current_stream(device)
+        key = (device, stream.cuda_stream, dtype, B, H, D, order, algo, split_select_gather,
+               tuple(segs))
+        entry = plan_cache.get(key)
+        if entry is None:
+            entry = _plan_plain(dtype, B, H, D, order, algo, segs)
+            if entry is None:  # rejected by kvc_plan (e.g. misaligned): general path reports
+                _run_general(device, dtype, B, H, D, js, out_list, order, algo, False, stream)
+                return
+            plan_cache.put(key, entry)
+        tmpl, info, ws, p, n_outs = entry
+        kos, vos, kops, vops = _outputs(device, dtype, B, H, D, n_outs)
+        table = tmpl.copy()
+        table["k"] = kps
+        table["v"] = vps
+        table["k_out"] = kops
+        table["v_out"] = vops
+        _launch(p, table, ws, info, stream, p.phases)
+        if _timer is not None and _timer.workspaces is not None:
+            _timer.workspaces.append((ws, info))
+    for j, ko, vo in zip(js, kos, vos):
+        out_list[j.layer_idx] = (ko, vo)
+
+
 def _run_group(device, dtype, B, H, D, js, out_list, order, algo):
-    n = len(js)
     external = any(j.ext_index is not None for j in js)
     if external and not all(j.ext_index is not None or j.n_select == 0 for j in js):
         raise RuntimeError("mixed external / engine-selected layers in one group")
+    with torch.cuda.device(device):
+        _run_general(device, dtype, B, H, D, js, out_list, order, algo, external,
+                     torch.cuda.current_stream(device))
+
+
+def _plan_plain(dtype, B, H, D, order, algo, segs):
+    """Planned table template of a plain-contiguous group (pointer columns zero), or None when
+    kvc_plan rejects it (the general path then reports the error)."""
+    table = np.zeros(len(segs), dtype=N.LAYER_DTYPE)
+    arr = np.array(segs, dtype=np.int64).reshape(len(segs), 9)
+    S = arr[:, 0]
+    st = np.stack([H * S * D, S * D, np.full_like(S, D)], axis=1)
+    table["k_stride"] = st
+    table["v_stride"] = st
+    for c, name in enumerate(("seq_len", "zone_start", "zone_len", "n_select", "sink_len",
+                              "tail_start", "tail_len", "pool_kernel", "score_mode")):
+        table[name] = arr[:, c]
+    n_outs = [int(x) for x in arr[:, 4] + arr[:, 3] + arr[:, 6]]
+    # plan with stand-in 16-B aligned pointers: the real ones are checked at launch
+    for name in ("k", "v", "k_out", "v_out"):
+        table[name] = 256
+    p = _params(dtype, B, H, D, order, algo, False)
+    rc, info = N.plan(p, table)
+    if rc != 0:
+        return None
+    for name in ("k", "v", "k_out", "v_out"):
+        table[name] = 0
+    ws = torch.empty(max(int(info.workspace_bytes), 256), dtype=torch.uint8,
+                     device=torch.cuda.current_device())
+    return table, info, ws, p, n_outs
+
+
+def _run_general(device, dtype, B, H, D, js, out_list, order, algo, external, stream):
     es = _ESIZE[dtype]
     rows_ok = (D * es) % 16 == 0
     n_outs = [j.sink_len + j.n_select + j.tail_len for j in js]
-    if all(x == n_outs[0] for x in n_outs):
-        # one allocation for every output of the call (decode steps: 64 tensors per token);
-        # each layer's K / V is a disjoint contiguous view of it
-        buf = torch.empty((2 * n, B, H, n_outs[0], D), dtype=dtype, device=device)
-        o = buf.unbind(0)
-        kos, vos = o[:n], o[n:]
-        base, step = buf.data_ptr(), B * H * n_outs[0] * D * es
-        kops = [base + i * step for i in range(n)]
-        vops = [base + (n + i) * step for i in range(n)]
-    else:
-        kos = [torch.empty((B, H, x, D), dtype=dtype, device=device) for x in n_outs]
-        vos = [torch.empty((B, H, x, D), dtype=dtype, device=device) for x in n_outs]
-        kops = [t.data_ptr() for t in kos]
-        vops = [t.data_ptr() for t in vos]
+    kos, vos, kops, vops = _outputs(device, dtype, B, H, D, n_outs)
     # one pass per layer: pointers, strides, segment bounds (inputs that are not plain
     # contiguous 16-B aligned rows go through _prep; prepared copies stay alive in `keep`)
     rows, keep = [], []
@@ -194,25 +331,17 @@ def _run_group(device, dtype, B, H, D, js, out_list, order, algo):
             vp = v.data_ptr()
             keep.append(v)
         kst, vst = k.stride(), v.stride()
-        rows.append((kp, vp, kops[i], vops[i], kst[:3], vst[:3], k.shape[2], j.zone_start,
-                     j.zone_len, j.n_select, j.sink_len, j.tail_start, j.tail_len,
+        rows.append((kp, vp, int(kops[i]), int(vops[i]), kst[:3], vst[:3], k.shape[2],
+                     j.zone_start, j.zone_len, j.n_select, j.sink_len, j.tail_start, j.tail_len,
                      j.pool_kernel, j.score_mode, 0, 0, 0, 0))
     table = np.array(rows, dtype=N.LAYER_DTYPE)
-
-    def params():
-        return N.Params(dtype=_SUPPORTED[dtype], batch=B, heads=H, head_dim=D, order=order,
-                        algo=algo, phases=N.PHASE_GATHER if external else N.PHASE_ALL,
-                        external_index=1 if external else 0,
-                        flags=N.FLAG_SPLIT_SELECT_GATHER if split_select_gather else 0)
-
     # One launch (score, select, gather kernels) for every layer of the group.  (Pipelining
     # layer chunks over two streams -- score of chunk c+1 beside select of chunk c -- was
     # measured slower at 2/4/8 chunks: profiles/r01_pipeline_sweep.json.)
-    with torch.cuda.device(device):
-        p = params()
-        ws, info = _upload(p, table, device, js, B, H)
-        _launch(p, table, ws, info, torch.cuda.current_stream(device), p.phases)
-        if _timer is not None and _timer.workspaces is not None:
-            _timer.workspaces.append((ws, info))
+    p = _params(dtype, B, H, D, order, algo, external)
+    ws, info = _upload(p, table, device, js, B, H)
+    _launch(p, table, ws, info, stream, p.phases)
+    if _timer is not None and _timer.workspaces is not None:
+        _timer.workspaces.append((ws, info))
     for j, ko, vo in zip(js, kos, vos):
         out_list[j.layer_idx] = (ko, vo)
