@@ -140,6 +140,27 @@ def test_abi_select_lengths(S):
         np.testing.assert_array_equal(idx, ref)
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("variant", ["normal", "few", "equal", "special"])
+def test_abi_decode_tail_selections(dtype, variant):
+    """Per-token decode shapes (S = cache + 1, one position evicted: k = n - 1) and the other
+    tail selections where 16-bit keys try the untied fast path before the chain (k or n - k
+    <= 64 on rows of <= 4096 positions), on both sides of that gate; tied maxima / minima
+    ('few', 'equal') must fall back to the chain."""
+    for S in (65, 257, 481, 513, 1025):
+        K = prng.gen_keys(4242 + S, (1, 3, S, 128), dtype, variant)
+        for k in sorted({1, 2, 63, 64, 65, S - 66, S - 65, S - 64, S - 2, S - 1}):
+            if not 0 < k < S:
+                continue
+            for desc in (0, 1):
+                nrm, idx = _abi_select(K, k, desc, 0)
+                ref = np.sort(oracle.argsort_prefix(nrm, k, descending=bool(desc)), axis=-1)
+                np.testing.assert_array_equal(idx, ref, err_msg=f"S={S} sort k={k} desc={desc}")
+            nrm, idx = _abi_select(K, k, 1, 1)
+            ref = np.sort(oracle.topk_indices(nrm, k), axis=-1)
+            np.testing.assert_array_equal(idx, ref, err_msg=f"S={S} topk k={k}")
+
+
 def test_random_strategy_matches_torch_restatement():
     """strategy='random' consumes torch's device RNG exactly like the reference."""
     from kvcompress.methods import fix_size_l2_compress

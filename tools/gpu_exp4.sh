@@ -1,0 +1,9 @@
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu.log
+for S in 513 16384; do AB_S=$S AB_DTYPE=bf16 timeout -k 10 200 python tools/phase_ab.py 2>/dev/null || exit $?; done
+timeout -k 10 300 python tools/decode_bench.py 2>/dev/null > gpurun_out/decode.json || exit $?
+cat gpurun_out/decode.json
+HOST_PROFILE_CALLS=200 timeout -k 10 200 python tools/host_profile.py 2>/dev/null | head -1
