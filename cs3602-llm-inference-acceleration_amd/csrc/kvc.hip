@@ -405,6 +405,30 @@ __device__ __forceinline__ void group_sync() {
     __syncthreads();
 }
 
+// The final insertion sort of a <= 64-element segment [lo, hi) (std::__insertion_sort /
+// __unguarded_linear_insert: an element moves left only past strictly greater ones, i.e. a
+// STABLE sort by key) computed by one wave in parallel: lane i holds element i and stores it at
+// #{key_j < key_i} + #{j < i : key_j == key_i}.  Every lane reads its element before any lane
+// of the wave stores (the ranks need all of them), so the in-place stores are race-free.
+// Replaces a one-lane loop of dependent LDS accesses.  Call with all 64 lanes of one wave.
+template <typename KeyT>
+__device__ __forceinline__ void wave_stable_sort(KeyT* key, uint16_t* idx, int lo, int hi) {
+  const int lane = threadIdx.x & 63;
+  const int m = hi - lo;
+  const bool own = lane < m;
+  const uint32_t kk = own ? (uint32_t)key[lo + lane] : 0u;
+  const uint16_t ii = own ? idx[lo + lane] : (uint16_t)0;
+  int r = 0;
+  for (int j = 0; j < m; ++j) {  // m is wave-uniform
+    const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)kk, j);
+    r += (kj < kk || (kj == kk && j < lane)) ? 1 : 0;
+  }
+  if (own) {
+    key[lo + r] = (KeyT)kk;
+    idx[lo + r] = ii;
+  }
+}
+
 // The partition chain of libstdc++ introsort (topk = false) / introselect (topk = true),
 // following only the segment [lo, hi) that straddles position k, run by NT cooperating lanes
 // (the whole 1024-thread block, or one wave once the segment is short).  One level is
@@ -654,7 +678,7 @@ __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, uint16_t* gpo
   while (true) {
     if (lo == k || hi == k) return 0;  // a partition boundary sits at k: the set is final
     if (hi - lo <= thr) {              // final (stable) insertion sort of the segment
-      if (tid == 0) insertion_sort(key, idx, lo, hi);
+      if (tid < 64) wave_stable_sort(key, idx, lo, hi);
       group_sync<NT>();
       return 0;
     }
