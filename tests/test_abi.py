@@ -35,6 +35,17 @@ def test_struct_layout():
     assert L.kvc_max_zone_len() == 1 << 24
 
 
+def test_integration_stub_matches_abi():
+    """The ctypes stub INTEGRATION.md offers a maintainer has kvc_params_t's fields, in order,
+    and the layer layout of _native (which is checked against the library above)."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    m = re.search(r"class Params\(ctypes\.Structure\):.*?\((.*?)\)\]", doc, flags=re.S)
+    names = re.findall(r'"(\w+)"', m.group(1))
+    assert names == [f[0] for f in N.Params._fields_]
+    layer = re.search(r"LAYER = np\.dtype\(\[(.*?)\]\)", doc, flags=re.S).group(1)
+    assert re.findall(r'\("(\w+)"', layer) == list(N.LAYER_DTYPE.names)
+
+
 def _layer(S, zs, zl, k, sink=0, ts=0, tl=0, ptr=4096):
     t = np.zeros(1, dtype=N.LAYER_DTYPE)[0]
     t["k"] = t["v"] = t["k_out"] = t["v_out"] = ptr

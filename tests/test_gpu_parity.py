@@ -213,6 +213,35 @@ def test_headline_geometry_32_layers(launch_path):
         assert ko.shape == (1, 32, 512, 128) and vo.shape == (1, 32, 512, 128)
 
 
+def test_repeated_call_shapes_reuse_plan_safely():
+    """Decode-step pattern: the same call shape many times (plan + workspace from the engine's
+    plan cache), each call with new K/V; every call's outputs -- all kept alive -- match the
+    oracle, also when calls alternate between two streams (one cached workspace per stream)."""
+    from kvcompress import _engine
+    from kvcompress.methods import fix_size_l2_compress, snapkv_lite_compress
+    _engine.plan_cache.clear()
+    side = torch.cuda.Stream()
+    kept = []
+    for step in range(6):
+        layers_np = [(prng.gen_keys(500 + 10 * step + i, (1, 4, 300, 64), "bf16", "few"),
+                      prng.gen_values(500 + 10 * step + i, (1, 4, 300, 64), "bf16"))
+                     for i in range(3)]
+        tin = [(to_dev(k), to_dev(v)) for k, v in layers_np]
+        with torch.cuda.stream(side if step % 2 else torch.cuda.current_stream()):
+            out_f = fix_size_l2_compress(list(tin), fix_kv_size=128, skip_layers=[])
+            out_s = snapkv_lite_compress(list(tin), observation_window=16, keep_size=100)
+        kept.append((layers_np, out_f, out_s))
+    torch.cuda.synchronize()
+    assert len(_engine.plan_cache.entries) == 4  # 2 shapes x 2 streams
+    for layers_np, out_f, out_s in kept:
+        for out, ref in ((out_f, oracle.fix_size_l2_compress(layers_np, fix_kv_size=128,
+                                                             skip_layers=[])),
+                         (out_s, oracle.snapkv_lite_compress(layers_np, observation_window=16,
+                                                             keep_size=100))):
+            for (ko, vo), (rk, rv, _) in zip(out, ref):
+                assert np.array_equal(to_np(ko), rk) and np.array_equal(to_np(vo), rv)
+
+
 def test_no_cpu_fallback():
     from kvcompress.methods import fix_size_l2_compress
     K = torch.zeros(1, 2, 100, 64, dtype=torch.bfloat16)
