@@ -34,8 +34,13 @@ constexpr int kScoreThreads = 256;
 constexpr int kScoreWaves = kScoreThreads / 64;
 constexpr int kSelThreads = 1024;
 constexpr int kSelWaves = kSelThreads / 64;
-constexpr int kSelThreadsSmall = 256;  // select workgroup for zones of up to kSmallZone
-constexpr int kSmallZone = kSelThreadsSmall * 16;
+// Zones of up to kSmallZone positions select with 512-thread workgroups and LDS sized by the
+// call's longest zone: all 1 024 rows of a 32-layer call are resident at once (4 per CU), and a
+// row's copy phase has 8 waves of loads in flight (256-thread rows: SELECT_GATHER 0.129 ms at
+// S = 4 096, 0.104 ms at S = 513; 512: 0.115 / 0.096).  Longer zones keep 1 024 threads (512
+// measured slower at 8 192 positions: 0.157 vs 0.147 ms).
+constexpr int kSelThreadsSmall = 512;
+constexpr int kSmallZone = 4096;
 constexpr int kZoneMax = 16384;        // longest zone whose selection runs from LDS
 constexpr int kZoneMaxGlobal = 65536;  // longest zone of the u16-position global variant
 constexpr int kZoneMaxLong = 1 << 24;   // longest zone at all (u32 positions; global scratch)
