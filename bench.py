@@ -402,8 +402,11 @@ def main():
         es = layers[0][0].element_size() if layers else 2
         nbytes = job_bytes(capture_jobs(step), es)
         # per-kernel durations: the engine splits each launch into its kernels with HIP events
-        # (recorded on the stream they run on) for the whole timed region
-        timer = _engine.PhaseTimer()
+        # (recorded on the stream they run on) for the whole timed region.  The events are
+        # created with hipEventDisableSystemFence: recording torch's default events between the
+        # kernels writes back / invalidates caches and cost the step 1.5-2.3 %, these ~1 %
+        # (tools/timer_overhead.py, profiles/r02_timer_overhead.json)
+        timer = _engine.PhaseTimer(fenceless=True)
     elapsed = timed_steps(step, args.steps, args.warmup, dist, sync, dev,
                           on_start=(lambda: _engine.set_phase_timer(timer)) if timer else None)
     if timer:
