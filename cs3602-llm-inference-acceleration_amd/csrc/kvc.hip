@@ -402,6 +402,155 @@ __device__ void snapkv_keys(const char* nrow, int n, int pool_k, bool desc, KeyT
   }
 }
 
+// x / 5 correctly rounded (= the IEEE division avg_pool1d performs), without the division
+// sequence: q0 = x * RN(1/5), residual r = x - 5 q0 exact in one FMA, q1 = q0 + r * RN(1/5);
+// q0 itself where r == 0 (keeps -0) or q0 is infinite.  Checked against x / 5.0f for all 2^32
+// fp32 patterns (tests/native/div5_check.c; tests/test_native_abi.py runs a strided sample).
+__device__ __forceinline__ float div5_rn(float x) {
+  const float q0 = x * 0.2f;
+  const float r = __builtin_fmaf(-q0, 5.0f, x);
+  return (r == 0.0f || __builtin_isinf(q0)) ? q0 : __builtin_fmaf(r, 0.2f, q0);
+}
+
+// snapkv_keys for 16-bit scores on LDS rows (n <= MAXV * 8 * NT): the same arithmetic per
+// position, with the row's norms read once as 16-B vectors (kept in registers for the max and
+// the scores), scores stored as 16-B vectors, and -- for the default pooling kernel 5 (and no
+// pooling) -- each thread pooling 8 consecutive positions from three 16-B reads of the scores
+// (the window sums add the same terms in the same order; terms outside [hs, he) are skipped).
+// Other pooling kernels pool one position at a time as snapkv_keys does.  `key`, `tmp` and
+// `nrow` are 16-B aligned; norm rows are padded to a multiple of 64 elements.
+template <int DT, int NT, int MAXV>
+__device__ __forceinline__ void snapkv_keys16(const char* nrow, int n, int pool_k, bool desc, uint16_t* key,
+                              uint16_t* tmp, SelScalars<uint16_t>& sc,
+                              uint64_t* stamps = nullptr) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nvec = (n + 7) >> 3;
+  uint4 raw[MAXV];
+  float mx = -__builtin_huge_valf();
+  int has_nan = 0;
+#pragma unroll
+  for (int q = 0; q < MAXV; ++q) {
+    const int v = tid + q * NT;
+    raw[q] = v < nvec ? reinterpret_cast<const uint4*>(nrow)[v] : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int q = 0; q < MAXV; ++q) {
+    const int v = tid + q * NT;
+    const uint32_t w[4] = {raw[q].x, raw[q].y, raw[q].z, raw[q].w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const uint32_t u = (w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+      const float f = DT == KVC_BF16 ? bf16_to_f32(u) : f16_to_f32(u);
+      if (v < nvec && v * 8 + e < n) {
+        if (f != f) has_nan = 1;
+        else if (f > mx) mx = f;
+      }
+    }
+  }
+  KVC_STAMP(26);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float y = __shfl_xor(mx, o, 64);
+    mx = y > mx ? y : mx;
+    has_nan |= __shfl_xor(has_nan, o, 64);
+  }
+  if (lane == 0) {
+    sc.fmax[wid] = mx;
+    sc.fnan[wid] = has_nan;
+  }
+  __syncthreads();
+  mx = sc.fmax[0];
+  has_nan = sc.fnan[0];
+  for (int w = 1; w < NT / 64; ++w) {
+    mx = sc.fmax[w] > mx ? sc.fmax[w] : mx;
+    has_nan |= sc.fnan[w];
+  }
+  if (has_nan) mx = __builtin_nanf("");
+  // `max + 1e-6` (snapkv_lite.py:99): the python scalar takes the tensor's dtype first
+  const float m = round_dt<DT>(mx + round_dt<DT>(1e-6f));
+  KVC_STAMP(27);
+#pragma unroll
+  for (int q = 0; q < MAXV; ++q) {
+    const int v = tid + q * NT;
+    if (v >= nvec) continue;
+    const uint32_t w[4] = {raw[q].x, raw[q].y, raw[q].z, raw[q].w};
+    uint32_t o[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      uint32_t pk = 0;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const uint32_t u = (w[h] >> (16 * b)) & 0xFFFFu;
+        const float f = DT == KVC_BF16 ? bf16_to_f32(u) : f16_to_f32(u);
+        pk |= (v * 8 + 2 * h + b < n ? bits16_dt<DT>(round_dt<DT>(m - f)) : 0u) << (16 * b);
+      }
+      o[h] = pk;
+    }
+    reinterpret_cast<uint4*>(tmp)[v] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+  __syncthreads();
+  KVC_STAMP(28);
+  const bool pool = pool_k > 1 && n >= pool_k;
+  if (pool && pool_k != 5) {  // other kernels: one position at a time (snapkv_keys)
+    const int pad = pool_k / 2;
+    for (int i = tid; i < n; i += NT) {
+      int hs = i - pad;
+      int he = min(hs + pool_k, n + pad);
+      const int psize = he - hs;
+      hs = max(hs, 0);
+      he = min(he, n);
+      float sum = 0.f;
+      for (int j = hs; j < he; ++j) sum = sum + load_dt<DT>(reinterpret_cast<char*>(tmp), j);
+      key[i] = key_of<DT>(sum / (float)psize, desc);
+    }
+    return;
+  }
+  const uint4* tv = reinterpret_cast<const uint4*>(tmp);
+#pragma unroll
+  for (int q = 0; q < MAXV; ++q) {
+    const int v = tid + q * NT;
+    if (v >= nvec) continue;
+    // scores of positions 8v - 8 .. 8v + 15 (zero outside the row: never summed)
+    float sw[24];
+    const uint4 c3[3] = {v > 0 ? tv[v - 1] : make_uint4(0, 0, 0, 0), tv[v],
+                         v + 1 < nvec ? tv[v + 1] : make_uint4(0, 0, 0, 0)};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const uint32_t w[4] = {c3[c].x, c3[c].y, c3[c].z, c3[c].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t u = (w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+        sw[c * 8 + e] = DT == KVC_BF16 ? bf16_to_f32(u) : f16_to_f32(u);
+      }
+    }
+    uint32_t o[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int i = v * 8 + e;
+      float r;
+      if (pool) {  // pool_k == 5, pad 2: window [i - 2, i + 3) clipped to [0, n), / 5
+        int hs = i - 2;
+        int he = min(hs + 5, n + 2);
+        const int psize = he - hs;
+        hs = max(hs, 0);
+        he = min(he, n);
+        float sum = 0.f;
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+          const int j = i - 2 + t;
+          if (j >= hs && j < he) sum = sum + sw[8 + e - 2 + t];
+        }
+        r = psize == 5 ? div5_rn(sum) : sum / (float)psize;
+      } else {
+        r = sw[8 + e];
+      }
+      o[e >> 1] |= (i < n ? (uint32_t)key_of<DT>(r, desc) : 0u) << (16 * (e & 1));
+    }
+    reinterpret_cast<uint4*>(key)[v] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+  KVC_STAMP(29);
+}
+
 template <int NT>
 __device__ __forceinline__ void group_sync() {
   if constexpr (NT == 64)
@@ -725,7 +874,7 @@ __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, uint16_t* gpo
                                                                acc);
 #ifdef KVC_STAMPS
     // per block level (first 8): cycles, and segment length  (slots 16.. of the row)
-    if (acc && NT > 64 && tid == 0 && level < 7) {
+    if (acc && NT > 64 && tid == 0 && level < 5) {
       acc[11 + 2 * level] = __builtin_amdgcn_s_memtime() - tl0;
       acc[12 + 2 * level] = acc[25];  // P1 | P2 << 20 | P4 << 40 of this level
     }
@@ -887,9 +1036,23 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
     // scratch for the unpooled scores from the idx region on: n u16 (bf16), or n floats over
     // idx + the rank tables (fp32 rows always get full n/2-rank tables: >= 4n bytes)
     char* tmp = reinterpret_cast<char*>(idx);
-    snapkv_keys<DT, KeyT, NT>(nrow, n, ly->pool_kernel, desc, key, tmp, sc);
-    __syncthreads();
-    for (int i = tid; i < n; i += NT) idx[i] = (uint16_t)i;
+    if constexpr (ESZ == 2 && MAXN <= kZoneMax) {
+      constexpr int MAXV = (MAXN / 8 + NT - 1) / NT;
+      snapkv_keys16<DT, NT, MAXV>(nrow, n, ly->pool_kernel, desc,
+                                  reinterpret_cast<uint16_t*>(key),
+                                  reinterpret_cast<uint16_t*>(tmp), sc, stamps);
+      __syncthreads();  // the scores (in the idx region) are dead
+      for (int v = tid; v < (n + 7) / 8; v += NT) {
+        const uint32_t b = (uint32_t)v * 8;
+        reinterpret_cast<uint4*>(idx)[v] =
+            make_uint4(b | (b + 1) << 16, (b + 2) | (b + 3) << 16, (b + 4) | (b + 5) << 16,
+                       (b + 6) | (b + 7) << 16);
+      }
+    } else {
+      snapkv_keys<DT, KeyT, NT>(nrow, n, ly->pool_kernel, desc, key, tmp, sc);
+      __syncthreads();
+      for (int i = tid; i < n; i += NT) idx[i] = (uint16_t)i;
+    }
   } else {
     // 16-B loads, all issued before the first use (norm rows are padded to 64 elements, so a
     // whole vector past n stays inside the row); keys/indices written as 16-B LDS stores
@@ -955,7 +1118,7 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
       accb = stamps + blockIdx.x * 32 + 5;
       accw = stamps + blockIdx.x * 32 + 10;
       if (tid == 0)
-        for (int q = 0; q < 27; ++q) accb[q] = 0;
+        for (int q = 0; q < 21; ++q) accb[q] = 0;
     }
 #endif
     const int st = run_chain<KeyT, NT, MAXJ>(key, idx, spos, A.gpos, sc, k, topk, thr, cap, lo,

@@ -46,3 +46,14 @@ def test_c_caller_fix_size_l2_matches_oracle(tmp_path, desc):
     rk, rv, _ = oracle.fix_size_l2_compress([(k, v)], fix_kv_size=K, keep_ratio=0.0,
                                             strategy=strategy, skip_layers=[])[0]
     assert np.array_equal(ko, rk.view(np.uint16)) and np.array_equal(vo, rv.view(np.uint16))
+
+
+def test_div5_matches_ieee_division():
+    """The snapkv pooling's x / 5 (csrc/kvc.hip div5_rn) equals IEEE x / 5.0f: every 61st of the
+    2^32 fp32 patterns here (all of them: `div5_check 1`, ~1 min)."""
+    src = os.path.join(ROOT, "tests", "native", "div5_check.c")
+    exe = os.path.join(ROOT, "tests", "native", "_build", "div5_check")
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", src, "-o", exe, "-lm"])
+    r = subprocess.run([exe, "61"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and " 0 mismatches" in r.stdout, r.stdout

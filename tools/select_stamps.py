@@ -16,8 +16,14 @@ from kvcompress import _native as N  # noqa: E402
 
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(0)
-L, H, S, D, k = 32, 32, 16384, 128, 512
-Ks = [torch.randn(1, H, S, D, device=dev, generator=g).to(torch.bfloat16) for _ in range(L)]
+L, H, D = 32, 32, 128
+S = int(os.environ.get("SEL_S", "16384"))
+k = int(os.environ.get("SEL_K", "512"))
+ALGO = int(os.environ.get("SEL_ALGO", "0"))      # 1: topk (introselect)
+ORDER = int(os.environ.get("SEL_ORDER", "0"))    # 1: descending
+SCORE = int(os.environ.get("SEL_SCORE", "0"))    # 1: snapkv scoring (pool 5)
+DT = {"bf16": (torch.bfloat16, N.KVC_BF16), "fp16": (torch.float16, N.KVC_F16)}[os.environ.get("SEL_DTYPE", "bf16")]
+Ks = [torch.randn(1, H, S, D, device=dev, generator=g).to(DT[0]) for _ in range(L)]
 table = np.zeros(L, dtype=N.LAYER_DTYPE)
 outs = []
 for i, K in enumerate(Ks):
@@ -28,12 +34,14 @@ for i, K in enumerate(Ks):
     t["k_out"] = t["v_out"] = o.data_ptr()
     t["k_stride"] = t["v_stride"] = K.stride()[:3]
     t["seq_len"], t["zone_start"], t["zone_len"], t["n_select"] = S, 0, S, k
-p = N.Params(dtype=N.KVC_BF16, batch=1, heads=H, head_dim=D, order=0, algo=0,
+    t["score_mode"], t["pool_kernel"] = SCORE, 5 if SCORE else 0
+p = N.Params(dtype=DT[1], batch=1, heads=H, head_dim=D, order=ORDER, algo=ALGO,
              phases=N.PHASE_SCORE | N.PHASE_SELECT, external_index=0)
 rc, info = N.plan(p, table)
 assert rc == 0
 ws = torch.zeros(int(info.workspace_bytes), dtype=torch.uint8, device=dev)
-res = {"wave_seg": "compile-time kWaveSeg"}
+res = {"wave_seg": "compile-time kWaveSeg", "S": S, "k": k, "algo": ALGO, "order": ORDER,
+       "score_mode": SCORE}
 for rep in range(3):
     rc = N.launch(p, table, ws.data_ptr(), int(info.workspace_bytes),
                   torch.cuda.current_stream().cuda_stream)
@@ -63,3 +71,11 @@ for q, nm in enumerate(("P1", "P2", "P4")):
     res["block_level_" + nm + "_median"] = [float(np.median((sp[:, i] >> (20 * q)) & 0xFFFFF))
                                             for i in range(7)]
 print(json.dumps(res))
+if os.environ.get("SEL_SNAP_STAMPS"):  # diagnostic: snapkv scoring phases (slots 26..29)
+    sn = allst[:, [1 - 1 + 1, 26, 27, 28, 29]]
+    ph = np.stack([allst[:, 26] - allst[:, 0], allst[:, 27] - allst[:, 26],
+                   allst[:, 28] - allst[:, 27], allst[:, 29] - allst[:, 28],
+                   allst[:, 1] - allst[:, 29]], axis=1)
+    print(json.dumps({"snapkv_phases_median": [float(np.median(ph[:, i])) for i in range(5)],
+                      "names": ["load+local max", "block max", "scores->tmp", "pool+keys",
+                                "idx init"]}))
