@@ -120,6 +120,23 @@ __device__ __forceinline__ typename DTypeTraits<DT>::key_t key_of(float f, bool 
     return key16_dt<DT>(bits16_dt<DT>(f), desc);
 }
 
+// Selection kernels are compiled per KEY CLASS (KC): KVC_BF16 stands for every 16-bit storage
+// dtype (u16 keys), KVC_F32 for fp32 (u32 keys).  bf16 and fp16 rows run the same binary with the
+// storage dtype as a runtime argument: the two differ only in the NaN threshold of the key map
+// and in the float conversions of the snapkv scores.  (Two instantiations of identical source
+// compiled ~2x apart in speed -- DESIGN.md "fp16 selection".)  f(integral_constant<int, DT>)
+// runs with the row's storage dtype.
+template <int KC, typename F>
+__device__ __forceinline__ void with_dt(int dt, F&& f) {
+  if constexpr (KC == KVC_F32)
+    f(std::integral_constant<int, KVC_F32>());
+  else if (dt == KVC_F16)
+    f(std::integral_constant<int, KVC_F16>());
+  else
+    f(std::integral_constant<int, KVC_BF16>());
+}
+__device__ __forceinline__ uint32_t inf_bits16(int dt) { return dt == KVC_F16 ? 0x7C00u : 0x7F80u; }
+
 // torch.gather's NaN rewrite on two 16-bit elements (bf16: 0xFFFF; fp16: quiet bit); fp32 none
 template <int DT>
 __device__ __forceinline__ uint4 canon_nan_dt(uint4 a) {
@@ -340,6 +357,20 @@ __device__ __forceinline__ uint64_t lanemask_le(int lane) {
   return lane == 63 ? ~0ull : ((1ull << (lane + 1)) - 1ull);
 }
 
+// 16-bit score conversions of the snapkv keys: bf16 by the c10 bit arithmetic, fp16 by the
+// hardware converts (kvc_common.h: c10-exact except NaN payloads, which the keys never see --
+// every NaN maps to the one NaN key).
+template <int DT>
+__device__ __forceinline__ float in16(uint32_t u) {
+  if constexpr (DT == KVC_BF16) return bf16_to_f32(u);
+  else return f16_to_f32_hw(u);
+}
+template <int DT>
+__device__ __forceinline__ uint32_t out16(float f) {
+  if constexpr (DT == KVC_BF16) return f32_to_bf16_rne(f);
+  else return f32_to_f16_hw(f);
+}
+
 // snapkv_lite importance scores (snapkv_lite.py:96-121) computed from the row's norms and
 // written as sort keys:  m = dt(max(norms) + 1e-6);  s = dt(m - norm);
 // pooled_i = dt(sum_{window} s / pool_size) (avg_pool1d, zero pad, count_include_pad).
@@ -440,7 +471,7 @@ __device__ __forceinline__ void snapkv_keys16(const char* nrow, int n, int pool_
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const uint32_t u = (w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
-      const float f = DT == KVC_BF16 ? bf16_to_f32(u) : f16_to_f32(u);
+      const float f = in16<DT>(u);
       if (v < nvec && v * 8 + e < n) {
         if (f != f) has_nan = 1;
         else if (f > mx) mx = f;
@@ -467,7 +498,7 @@ __device__ __forceinline__ void snapkv_keys16(const char* nrow, int n, int pool_
   }
   if (has_nan) mx = __builtin_nanf("");
   // `max + 1e-6` (snapkv_lite.py:99): the python scalar takes the tensor's dtype first
-  const float m = round_dt<DT>(mx + round_dt<DT>(1e-6f));
+  const float m = in16<DT>(out16<DT>(mx + in16<DT>(out16<DT>(1e-6f))));
   KVC_STAMP(27);
 #pragma unroll
   for (int q = 0; q < MAXV; ++q) {
@@ -481,8 +512,8 @@ __device__ __forceinline__ void snapkv_keys16(const char* nrow, int n, int pool_
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const uint32_t u = (w[h] >> (16 * b)) & 0xFFFFu;
-        const float f = DT == KVC_BF16 ? bf16_to_f32(u) : f16_to_f32(u);
-        pk |= (v * 8 + 2 * h + b < n ? bits16_dt<DT>(round_dt<DT>(m - f)) : 0u) << (16 * b);
+        const float f = in16<DT>(u);
+        pk |= (v * 8 + 2 * h + b < n ? out16<DT>(m - f) : 0u) << (16 * b);
       }
       o[h] = pk;
     }
@@ -500,8 +531,8 @@ __device__ __forceinline__ void snapkv_keys16(const char* nrow, int n, int pool_
       hs = max(hs, 0);
       he = min(he, n);
       float sum = 0.f;
-      for (int j = hs; j < he; ++j) sum = sum + load_dt<DT>(reinterpret_cast<char*>(tmp), j);
-      key[i] = key_of<DT>(sum / (float)psize, desc);
+      for (int j = hs; j < he; ++j) sum = sum + in16<DT>(tmp[j]);
+      key[i] = key16_dt<DT>(out16<DT>(sum / (float)psize), desc);
     }
     return;
   }
@@ -520,7 +551,7 @@ __device__ __forceinline__ void snapkv_keys16(const char* nrow, int n, int pool_
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const uint32_t u = (w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
-        sw[c * 8 + e] = DT == KVC_BF16 ? bf16_to_f32(u) : f16_to_f32(u);
+        sw[c * 8 + e] = in16<DT>(u);
       }
     }
     uint32_t o[4] = {0, 0, 0, 0};
@@ -544,7 +575,7 @@ __device__ __forceinline__ void snapkv_keys16(const char* nrow, int n, int pool_
       } else {
         r = sw[8 + e];
       }
-      o[e >> 1] |= (i < n ? (uint32_t)key_of<DT>(r, desc) : 0u) << (16 * (e & 1));
+      o[e >> 1] |= (i < n ? (uint32_t)key16_dt<DT>(out16<DT>(r), desc) : 0u) << (16 * (e & 1));
     }
     reinterpret_cast<uint4*>(key)[v] = make_uint4(o[0], o[1], o[2], o[3]);
   }
@@ -1004,14 +1035,14 @@ __device__ bool select_fast_untied(const KeyT* key, int n, int k, SelScalars<Key
 // global scratch row for zones longer than kZoneMax) and scalars in `sc`; NT threads (the
 // workgroup) cooperate.  Emits the kept zone-local indices in ascending order to `out` (global
 // int32) or, with TO_LDS, to `sel` (LDS u16, may alias the key region: keys are dead by then).
-template <int DT, bool TO_LDS, int MAXN, int NT>
-__device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, int order, int algo,
-                            const char* __restrict__ nrow, int32_t* out, uint16_t* sel,
+template <int KC, bool TO_LDS, int MAXN, int NT>
+__device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, int dt, int order,
+                            int algo, const char* __restrict__ nrow, int32_t* out, uint16_t* sel,
                             char* arrays, int n_cap, int cap,
-                            SelScalars<typename DTypeTraits<DT>::key_t>& sc,
+                            SelScalars<typename DTypeTraits<KC>::key_t>& sc,
                             int wave_seg, uint64_t* stamps) {
-  typedef typename DTypeTraits<DT>::key_t KeyT;
-  constexpr int ESZ = DTypeTraits<DT>::esz;
+  typedef typename DTypeTraits<KC>::key_t KeyT;
+  constexpr int ESZ = DTypeTraits<KC>::esz;
   constexpr int MAXJ = (MAXN + NT - 1) / NT;  // positions per lane, level 0
   const SelArrays<KeyT> A(arrays, n_cap, cap);
   KeyT* key = A.key;
@@ -1038,9 +1069,11 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
     char* tmp = reinterpret_cast<char*>(idx);
     if constexpr (ESZ == 2 && MAXN <= kZoneMax) {
       constexpr int MAXV = (MAXN / 8 + NT - 1) / NT;
-      snapkv_keys16<DT, NT, MAXV>(nrow, n, ly->pool_kernel, desc,
-                                  reinterpret_cast<uint16_t*>(key),
-                                  reinterpret_cast<uint16_t*>(tmp), sc, stamps);
+      with_dt<KC>(dt, [&](auto D) {
+        snapkv_keys16<D.value, NT, MAXV>(nrow, n, ly->pool_kernel, desc,
+                                         reinterpret_cast<uint16_t*>(key),
+                                         reinterpret_cast<uint16_t*>(tmp), sc, stamps);
+      });
       __syncthreads();  // the scores (in the idx region) are dead
       for (int v = tid; v < (n + 7) / 8; v += NT) {
         const uint32_t b = (uint32_t)v * 8;
@@ -1049,7 +1082,9 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
                        (b + 6) | (b + 7) << 16);
       }
     } else {
-      snapkv_keys<DT, KeyT, NT>(nrow, n, ly->pool_kernel, desc, key, tmp, sc);
+      with_dt<KC>(dt, [&](auto D) {
+        snapkv_keys<D.value, KeyT, NT>(nrow, n, ly->pool_kernel, desc, key, tmp, sc);
+      });
       __syncthreads();
       for (int i = tid; i < n; i += NT) idx[i] = (uint16_t)i;
     }
@@ -1072,11 +1107,12 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
       if (v < nvec) {
         const uint32_t w[4] = {buf[q].x, buf[q].y, buf[q].z, buf[q].w};
         uint32_t kw[4], iw[4];
-        if constexpr (DT != KVC_F32) {
+        if constexpr (KC != KVC_F32) {
+          const uint32_t inf = inf_bits16(dt);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            kw[e] = (uint32_t)key16_dt<DT>(w[e] & 0xFFFFu, desc) |
-                    ((uint32_t)key16_dt<DT>(w[e] >> 16, desc) << 16);
+            kw[e] = (uint32_t)key_h16(w[e] & 0xFFFFu, desc, inf) |
+                    ((uint32_t)key_h16(w[e] >> 16, desc, inf) << 16);
             iw[e] = (uint32_t)(v * 8 + 2 * e) | ((uint32_t)(v * 8 + 2 * e + 1) << 16);
           }
           *reinterpret_cast<uint4*>(key + v * 8) = make_uint4(kw[0], kw[1], kw[2], kw[3]);
@@ -1183,14 +1219,14 @@ constexpr int kSelCapBig = sel_cap(kZoneMax, (int)sizeof(KeyT));
 template <typename KeyT>
 constexpr int kSelBytesBig = (int)sel_bytes(kZoneMax, (int)sizeof(KeyT), kSelCapBig<KeyT>);
 
-template <int DT, int NT>
+template <int KC, int NT>
 __global__ void __launch_bounds__(NT, 8)  // 8 waves per SIMD: two 1024-thread rows per CU
-    select_kernel(const LayerChunk T, int BH, int order, int algo,
+    select_kernel(const LayerChunk T, int BH, int dt, int order, int algo,
                   const char* __restrict__ norms, int64_t norm_stride,
                   int32_t* __restrict__ out_idx, int64_t idx_stride, int wave_seg, int n_cap,
                   int cap, uint64_t* stamps) {
-  typedef typename DTypeTraits<DT>::key_t KeyT;
-  constexpr int ESZ = DTypeTraits<DT>::esz;
+  typedef typename DTypeTraits<KC>::key_t KeyT;
+  constexpr int ESZ = DTypeTraits<KC>::esz;
   constexpr int MAXN = NT == kSelThreads ? kZoneMax : NT * 16;
   __shared__ SelScalars<KeyT> sc;
   const kvc_layer_t* ly = T.l + blockIdx.x / BH;
@@ -1198,12 +1234,14 @@ __global__ void __launch_bounds__(NT, 8)  // 8 waves per SIMD: two 1024-thread r
   if constexpr (NT == kSelThreads) {
     // LDS: key[kZoneMax] | idx[kZoneMax] (u16) | spos | gpos (u16 rank windows) -- SelArrays
     __shared__ __attribute__((aligned(16))) char smem[kSelBytesBig<KeyT>];
-    select_body<DT, false, MAXN, NT>(ly, order, algo, norms + (int64_t)row * norm_stride * ESZ,
+    select_body<KC, false, MAXN, NT>(ly, dt, order, algo,
+                                     norms + (int64_t)row * norm_stride * ESZ,
                                      out_idx + (int64_t)row * idx_stride, nullptr, smem, kZoneMax,
                                      kSelCapBig<KeyT>, sc, wave_seg, stamps);
   } else {
     extern __shared__ __attribute__((aligned(16))) char dsmem[];
-    select_body<DT, false, MAXN, NT>(ly, order, algo, norms + (int64_t)row * norm_stride * ESZ,
+    select_body<KC, false, MAXN, NT>(ly, dt, order, algo,
+                                     norms + (int64_t)row * norm_stride * ESZ,
                                      out_idx + (int64_t)row * idx_stride, nullptr, dsmem, n_cap,
                                      cap, sc, wave_seg, stamps);
   }
@@ -1212,19 +1250,19 @@ __global__ void __launch_bounds__(NT, 8)  // 8 waves per SIMD: two 1024-thread r
 // Zones longer than kZoneMax (up to kZoneMaxGlobal): the same selection with its arrays in a
 // per-row global scratch (L2 / Infinity-Cache resident; a workgroup barrier orders the
 // workgroup's global accesses like LDS ones -- all its waves share one CU's L1).
-template <int DT>
+template <int KC>
 __global__ void __launch_bounds__(kSelThreads)
-    select_global_kernel(const LayerChunk T, int BH, int order, int algo,
+    select_global_kernel(const LayerChunk T, int BH, int dt, int order, int algo,
                          const char* __restrict__ norms, int64_t norm_stride,
                          int32_t* __restrict__ out_idx, int64_t idx_stride, int wave_seg,
                          char* __restrict__ scratch, int64_t scratch_row_bytes, int n_cap) {
-  typedef typename DTypeTraits<DT>::key_t KeyT;
-  constexpr int ESZ = DTypeTraits<DT>::esz;
+  typedef typename DTypeTraits<KC>::key_t KeyT;
+  constexpr int ESZ = DTypeTraits<KC>::esz;
   __shared__ SelScalars<KeyT> sc;
   const kvc_layer_t* ly = T.l + blockIdx.x / BH;
   const int row = ly->row0 + (int)(blockIdx.x % BH);
-  select_body<DT, false, kZoneMaxGlobal, kSelThreads>(
-      ly, order, algo, norms + (int64_t)row * norm_stride * ESZ,
+  select_body<KC, false, kZoneMaxGlobal, kSelThreads>(
+      ly, dt, order, algo, norms + (int64_t)row * norm_stride * ESZ,
       out_idx + (int64_t)row * idx_stride, nullptr, scratch + (int64_t)row * scratch_row_bytes,
       n_cap, n_cap / 2 + 1, sc, wave_seg, nullptr);
 }
@@ -1337,14 +1375,14 @@ __device__ int partition_long(KeyT* key, uint32_t* idx, uint32_t* spos, uint32_t
   return cut;
 }
 
-template <int DT>
+template <int KC>
 __global__ void __launch_bounds__(kSelThreads)
-    select_long_kernel(const LayerChunk T, int BH, int order, int algo,
+    select_long_kernel(const LayerChunk T, int BH, int dt, int order, int algo,
                        const char* __restrict__ norms, int64_t norm_stride,
                        int32_t* __restrict__ out_idx, int64_t idx_stride,
                        char* __restrict__ scratch, int64_t scratch_row_bytes, int n_cap) {
-  typedef typename DTypeTraits<DT>::key_t KeyT;
-  constexpr int ESZ = DTypeTraits<DT>::esz;
+  typedef typename DTypeTraits<KC>::key_t KeyT;
+  constexpr int ESZ = DTypeTraits<KC>::esz;
   __shared__ SelScalars<KeyT> ssc;
   __shared__ LongScalars sc;
   const kvc_layer_t* ly = T.l + blockIdx.x / BH;
@@ -1365,15 +1403,17 @@ __global__ void __launch_bounds__(kSelThreads)
   uint32_t* gpos = spos + (n_cap / 2 + 2);
   const bool desc = order == KVC_DESC;
   if (ly->score_mode == KVC_SCORE_SNAPKV) {  // unpooled scores in the idx region first
-    snapkv_keys<DT, KeyT, kSelThreads>(nrow, n, ly->pool_kernel, desc, key,
-                                       reinterpret_cast<char*>(idx), ssc);
+    with_dt<KC>(dt, [&](auto D) {
+      snapkv_keys<D.value, KeyT, kSelThreads>(nrow, n, ly->pool_kernel, desc, key,
+                                              reinterpret_cast<char*>(idx), ssc);
+    });
     __syncthreads();
   } else {
     for (int i = tid; i < n; i += kSelThreads) {
-      if constexpr (DT == KVC_F32)
-        key[i] = key_f32(f32_to_bits(load_dt<DT>(nrow, i)), desc);
+      if constexpr (KC == KVC_F32)
+        key[i] = key_f32(reinterpret_cast<const uint32_t*>(nrow)[i], desc);
       else
-        key[i] = key16_dt<DT>(reinterpret_cast<const uint16_t*>(nrow)[i], desc);
+        key[i] = key_h16(reinterpret_cast<const uint16_t*>(nrow)[i], desc, inf_bits16(dt));
     }
   }
   for (int i = tid; i < n; i += kSelThreads) idx[i] = (uint32_t)i;
@@ -1594,13 +1634,13 @@ __device__ __forceinline__ void gather_row(const kvc_layer_t* __restrict__ ly, i
 // bound), and the index list never round-trips through global memory.  Layout and thread
 // counts as select_kernel; rows without a selection only copy.
 // ---------------------------------------------------------------------------------------------
-template <int DT, int NT, int NC>
+template <int KC, int NT, int NC>
 __global__ void __launch_bounds__(NT, 8)
-    select_gather_kernel(const LayerChunk T, int H, int BH, int order, int algo,
+    select_gather_kernel(const LayerChunk T, int H, int BH, int dt, int order, int algo,
                          const char* __restrict__ norms, int64_t norm_stride, int wave_seg,
                          int n_cap, int cap) {
-  typedef typename DTypeTraits<DT>::key_t KeyT;
-  constexpr int ESZ = DTypeTraits<DT>::esz;
+  typedef typename DTypeTraits<KC>::key_t KeyT;
+  constexpr int ESZ = DTypeTraits<KC>::esz;
   constexpr int MAXN = NT == kSelThreads ? kZoneMax : NT * 16;
   __shared__ SelScalars<KeyT> sc;
   const kvc_layer_t* ly = T.l + blockIdx.x / BH;
@@ -1620,11 +1660,13 @@ __global__ void __launch_bounds__(NT, 8)
   }
   uint16_t* sel = reinterpret_cast<uint16_t*>(arrays);  // key region, dead after the chain
   if (selects) {
-    select_body<DT, true, MAXN, NT>(ly, order, algo, nrow, nullptr, sel, arrays, n_cap, cap, sc,
-                                    wave_seg, nullptr);
+    select_body<KC, true, MAXN, NT>(ly, dt, order, algo, nrow, nullptr, sel, arrays, n_cap, cap,
+                                    sc, wave_seg, nullptr);
     __syncthreads();
   }
-  gather_row<DT, NC, NT, true>(ly, r, H, selects ? sel : nullptr);
+  with_dt<KC>(dt, [&](auto D) {
+    gather_row<D.value, NC, NT, true>(ly, r, H, selects ? sel : nullptr);
+  });
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1783,6 +1825,7 @@ template <int DT, int NC>
 static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, const kvc_layer_t* layers,
                         int nl, int c0, int cn, char* w, hipStream_t s) {
   typedef typename DTypeTraits<DT>::key_t KeyT;
+  constexpr int KC = DT == KVC_F32 ? KVC_F32 : KVC_BF16;  // selection binary: the key class
   const int H = p->heads, BH = p->batch * p->heads;
   char* norms = w + info.norm_offset;
   int32_t* idx = reinterpret_cast<int32_t*>(w + info.index_offset);
@@ -1814,10 +1857,10 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
     char* scratch = w + round_up(info.index_offset + (size_t)info.rows * istride * 4, 256);
     const int64_t rb = (int64_t)sel_scratch_row_bytes(n_cap, p->dtype);
     if (n_cap > kZoneMaxGlobal)  // u32 positions (the call's longest zone decides)
-      rc = launch_k(select_long_kernel<DT>, rows_grid, dim3(kSelThreads), 0, s, T, BH, p->order,
-                    p->algo, norms, nstride, idx, istride, scratch, rb, n_cap);
+      rc = launch_k(select_long_kernel<KC>, rows_grid, dim3(kSelThreads), 0, s, T, BH, DT,
+                    p->order, p->algo, norms, nstride, idx, istride, scratch, rb, n_cap);
     else
-      rc = launch_k(select_global_kernel<DT>, rows_grid, dim3(kSelThreads), 0, s, T, BH,
+      rc = launch_k(select_global_kernel<KC>, rows_grid, dim3(kSelThreads), 0, s, T, BH, DT,
                     p->order, p->algo, norms, nstride, idx, istride, kWaveSeg, scratch, rb, n_cap);
   } else if ((p->phases & KVC_PHASE_SELECT) && sel && !ext) {
     uint64_t* st = stamps ? stamps + (size_t)layers[c0].row0 * 32 : nullptr;
@@ -1829,19 +1872,19 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
                          !(p->flags & KVC_FLAG_SPLIT_SELECT_GATHER);
     if (fuse_sg) {  // this chunk's gather happens inside the select kernel
       if (small)
-        return launch_k(select_gather_kernel<DT, kSelThreadsSmall, NC>, rows_grid,
-                        dim3(kSelThreadsSmall), lds, s, T, H, BH, p->order, p->algo, norms,
+        return launch_k(select_gather_kernel<KC, kSelThreadsSmall, NC>, rows_grid,
+                        dim3(kSelThreadsSmall), lds, s, T, H, BH, DT, p->order, p->algo, norms,
                         nstride, kWaveSeg, n_cap, cap);
-      return launch_k(select_gather_kernel<DT, kSelThreads, NC>, rows_grid, dim3(kSelThreads),
-                      lds, s, T, H, BH, p->order, p->algo, norms, nstride, kWaveSeg, n_cap, cap);
+      return launch_k(select_gather_kernel<KC, kSelThreads, NC>, rows_grid, dim3(kSelThreads),
+                      lds, s, T, H, BH, DT, p->order, p->algo, norms, nstride, kWaveSeg, n_cap, cap);
     }
     if (small)
-      rc = launch_k(select_kernel<DT, kSelThreadsSmall>, rows_grid, dim3(kSelThreadsSmall), lds,
-                    s, T, BH, p->order, p->algo, norms, nstride, idx, istride, kWaveSeg, n_cap,
+      rc = launch_k(select_kernel<KC, kSelThreadsSmall>, rows_grid, dim3(kSelThreadsSmall), lds,
+                    s, T, BH, DT, p->order, p->algo, norms, nstride, idx, istride, kWaveSeg, n_cap,
                     cap, st);
     else
-      rc = launch_k(select_kernel<DT, kSelThreads>, rows_grid, dim3(kSelThreads), lds, s, T, BH,
-                    p->order, p->algo, norms, nstride, idx, istride, kWaveSeg, n_cap, cap, st);
+      rc = launch_k(select_kernel<KC, kSelThreads>, rows_grid, dim3(kSelThreads), lds, s, T, BH,
+                    DT, p->order, p->algo, norms, nstride, idx, istride, kWaveSeg, n_cap, cap, st);
   }
   if (rc != KVC_OK) return rc;
   if ((p->phases & KVC_PHASE_GATHER) && max_out > 0)

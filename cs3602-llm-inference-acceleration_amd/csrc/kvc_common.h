@@ -68,6 +68,18 @@ KVC_HD uint32_t f32_to_f16_rne(float f) {
   return sign | r;
 }
 
+// The same two conversions with the hardware converts (v_cvt_f32_f16 / v_cvt_f16_f32: IEEE
+// round-to-nearest-even, fp16 denormals kept -- the gfx950 default mode).  Bit-identical to
+// f16_to_f32 / f32_to_f16_rne on every non-NaN input and NaN for every NaN input; only NaN
+// payloads may differ, so they serve where a NaN is only ever tested or mapped to a key (the
+// snapkv scores).  tests/native/cvt16_check.hip checks all 2^16 and 2^32 inputs on the GPU.
+__device__ __forceinline__ float f16_to_f32_hw(uint32_t h) {
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)h);
+}
+__device__ __forceinline__ uint32_t f32_to_f16_hw(float f) {
+  return __builtin_bit_cast(uint16_t, (_Float16)f);
+}
+
 // Sort keys.  Ascending base order is PyTorch's asc comparator
 //   (!isnan(a) && isnan(b)) || a < b
 // i.e. numeric order with -0 == +0 and every NaN tied above +inf.  Descending order

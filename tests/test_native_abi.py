@@ -57,3 +57,14 @@ def test_div5_matches_ieee_division():
     subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", src, "-o", exe, "-lm"])
     r = subprocess.run([exe, "61"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and " 0 mismatches" in r.stdout, r.stdout
+
+
+@pytest.mark.gpu
+def test_hw_fp16_converts_match_c10():
+    """The hardware fp16 converts of the snapkv scoring (kvc_common.h f16_to_f32_hw /
+    f32_to_f16_hw) against the c10-exact conversions for all 2^16 and all 2^32 inputs
+    (tests/native/cvt16_check.hip, built by __graft_entry__.build())."""
+    exe = os.path.join(ROOT, "tests", "native", "_build", "cvt16_check")
+    assert os.path.exists(exe), "run __graft_entry__.build() first"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "\n0 mismatches" in "\n" + r.stdout.splitlines()[-1], r.stdout
