@@ -661,12 +661,102 @@ __device__ __forceinline__ int mbcnt(uint64_t mask, int base) {
                                         __builtin_amdgcn_mbcnt_lo((uint32_t)mask, (uint32_t)base));
 }
 
+// f(integral_constant<int, I>) for I in [B, E): a loop the compiler cannot leave rolled.
+template <int B, int E, typename F>
+__device__ __forceinline__ void unroll_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>());
+    unroll_for<B + 1, E>(f);
+  }
+}
+
+// P1 of a level: the ge / le counts of one wave's stripe, wave-uniform from the compare ballots
+// (s_bcnt on the scalar unit; no per-lane flag state).  WHOLE: every position of the stripe is
+// below hi (unclamped loads with immediate offsets; rows j >= J of a JM-row body read at most
+// JM/2 rows past the stripe, inside the selection arrays).  Otherwise loads are clamped and
+// lanes past hi masked off.  Position ch is counted with the key it holds (the pivot value);
+// the caller corrects the owner wave's counts for the virtual median move.
+template <typename KeyT, int JM, bool WHOLE>
+__device__ __forceinline__ void p1_counts(const KeyT* key, int pos0, int J, int hi, uint32_t p,
+                                          int& cge, int& cle) {
+  constexpr int JB = JM < 16 ? JM : 16;
+  unroll_for<0, JM / JB>([&](auto bc) {
+    constexpr int j0 = decltype(bc)::value * JB;
+    if (j0 > 0 && j0 >= J) return;
+    KeyT kv[JB];
+    unroll_for<0, JB>([&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+      const int pos = pos0 + (j0 + q) * 64;
+      kv[q] = key[WHOLE ? pos : min(pos, hi - 1)];
+    });
+    unroll_for<0, JB>([&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+      constexpr int j = j0 + q;
+      if (j >= JM / 2 && j >= J) return;
+      bool ge = (uint32_t)kv[q] >= p, le = (uint32_t)kv[q] <= p;
+      if constexpr (!WHOLE) {
+        const bool inb = pos0 + j * 64 < hi;
+        ge = ge && inb;
+        le = le && inb;
+      }
+      cge += __popcll(__builtin_amdgcn_ballot_w64(ge));
+      cle += __popcll(__builtin_amdgcn_ballot_w64(le));
+    });
+  });
+}
+
+// P2 of a level, rank window 0: scatter the s and g rank -> position tables for ranks <= cap
+// (every ge position: g_{m+1} is then read from the table) and count the swaps (nsw), from
+// re-read keys.
+// FAST: a whole stripe without the median slot.  Otherwise lanes past hi are masked and the
+// median slot ch carries klo's flags (kge / kle): the owner wave moves the median physically
+// only after this pass.
+template <typename KeyT, int JM, bool FAST>
+__device__ __forceinline__ void p2_window0(const KeyT* key, uint16_t* spos, uint16_t* gpos,
+                                           int lane, int pos0, int wbeg, int J, int hi,
+                                           uint32_t p, int ch, bool kge, bool kle, int rge1,
+                                           int rle, int tot_le, int cap, int& nsw) {
+  constexpr int JB = JM < 8 ? JM : 8;  // keys in flight per lane (register budget: 64 VGPRs)
+  const int t1 = tot_le + 1;
+  unroll_for<0, JM / JB>([&](auto bc) {
+    constexpr int j0 = decltype(bc)::value * JB;
+    if (j0 > 0 && j0 >= J) return;
+    KeyT kv[JB];
+    unroll_for<0, JB>([&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+      const int pos = pos0 + (j0 + q) * 64;
+      kv[q] = key[FAST ? pos : min(pos, hi - 1)];
+    });
+    unroll_for<0, JB>([&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+      constexpr int j = j0 + q;
+      if (j >= JM / 2 && j >= J) return;
+      const int pj = pos0 + j * 64;
+      bool ge = (uint32_t)kv[q] >= p, le = (uint32_t)kv[q] <= p;
+      if constexpr (!FAST) {
+        const bool inb = pj < hi, isch = pj == ch;
+        ge = inb && (isch ? kge : ge);
+        le = inb && (isch ? kle : le);
+      }
+      const uint64_t bg = __builtin_amdgcn_ballot_w64(ge), bl = __builtin_amdgcn_ballot_w64(le);
+      const int a1 = mbcnt(bg, rge1);                   // g rank: A + 1
+      const int sr = t1 - (mbcnt(bl, rle) + (le ? 1 : 0));  // s rank: tot_le - Lin + 1
+      spos[(le && sr <= cap) ? sr : lane - 64] = (uint16_t)pj;
+      gpos[(ge && a1 <= cap) ? a1 : lane - 64] = (uint16_t)pj;
+      // g_t < s_t  <=>  A + Lin < tot_le  <=>  a1 < sr: swapped (a prefix t <= m of the g's)
+      nsw += __popcll(bg & __builtin_amdgcn_ballot_w64(a1 < sr));
+      rge1 += __popcll(bg);
+      rle += __popcll(bl);
+    });
+  });
+}
+
 // One partition level over [lo, hi) with at most JM positions per lane (compile-time bound; the
 // passes stop at the segment's own J with a scalar branch).  Returns cut.  See run_chain for
-// the algorithm.  The level is issue-bound (every wave executes its bookkeeping), so all
-// wave-uniform work -- median of 3, cross-wave prefix sums, swap count, g_{m+1} -- runs on
-// SGPRs (readfirstlane / readlane / ballot popcounts) and per-position work is ~30 VALU per
-// 64 positions.
+// the algorithm.  P1 and P2 are issue-bound at the long levels (16 waves of 16 rows of 64
+// positions), so per-position work is a handful of VALU ops: flags are compare ballots
+// (recomputed from the keys in P2 rather than carried), wave counts are scalar popcounts, and
+// wave-uniform work -- median of 3, cross-wave prefix sums, swap count, g_{m+1} -- runs on SGPRs.
 template <typename KeyT, int NT, int JM>
 __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_t* spos,
                                                uint16_t* gpos, SelScalars<KeyT>& sc, int lo,
@@ -682,7 +772,7 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
   const int wbeg = lo + 1 + wid * J * 64;
   const int pos0 = wbeg + lane;
   // ---- median of 3 (std::__move_median_to_first), on the scalar unit; the swap into lo is
-  // virtual until P2 ----
+  // virtual until the owner wave of position ch has read its P2 keys ----
   const int a = lo + 1, b = lo + (hi - lo) / 2, c = hi - 1;
   const uint32_t ka = (uint32_t)uni((int)key[a]), kb = (uint32_t)uni((int)key[b]);
   const uint32_t kc = (uint32_t)uni((int)key[c]), klo = (uint32_t)uni((int)key[lo]);
@@ -697,96 +787,98 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
     ch = b;
   }
   const uint32_t p = (ch == a) ? ka : (ch == b) ? kb : kc;
-  // ---- P1: ge/le flags (one bit per j in gem/lem), wave counts ----
-  MaskT gem = 0, lem = 0;
-  constexpr int JB = JM < 16 ? JM : 16;  // keys loaded in batches of JB per lane
-#pragma unroll
-  for (int j0 = 0; j0 < JM; j0 += JB) {
-    if (j0 >= J) break;
-    uint32_t kv[JB];
-#pragma unroll
-    for (int q = 0; q < JB; ++q) kv[q] = (uint32_t)key[min(pos0 + (j0 + q) * 64, hi - 1)];
-#pragma unroll
-    for (int q = 0; q < JB; ++q) {
-      const int j = j0 + q;
-      if (j >= J) break;
-      const int pos = pos0 + j * 64;
-      const bool inb = pos < hi;
-      const uint32_t kk = (pos == ch) ? klo : kv[q];
-      gem |= (inb && kk >= p) ? ((MaskT)1 << j) : (MaskT)0;
-      lem |= (inb && kk <= p) ? ((MaskT)1 << j) : (MaskT)0;
-    }
+  const bool kge = klo >= p, kle = klo <= p;  // flags of the key that moves into slot ch
+  const int nval = hi - wbeg;                 // positions of this wave's stripe below hi
+  const bool whole = nval >= J * 64;
+  const bool owner = ch >= wbeg && ch < wbeg + J * 64;
+  uint64_t ta = 0, tb = 0, tc = 0;  // diagnostic build: P1 sub-phases of a J = 16 level
+  KVC_TICK(ta);
+  // ---- P1: wave ge / le counts ----
+  int cge = 0, cle = 0;
+  if (whole)
+    p1_counts<KeyT, JM, true>(key, pos0, J, hi, p, cge, cle);
+  else if (nval > 0)
+    p1_counts<KeyT, JM, false>(key, pos0, J, hi, p, cge, cle);
+  if (owner) {  // slot ch was counted with the pivot's flags (both set); it holds klo
+    cge -= kge ? 0 : 1;
+    cle -= kle ? 0 : 1;
   }
-  // wave counts: per-lane popcounts, one packed 64-lane sum (row scans + 4 readlanes)
-  const int rs = row_scan16(__popcll((uint64_t)gem) | (__popcll((uint64_t)lem) << 16));
-  const int cnt = __builtin_amdgcn_readlane(rs, 15) + __builtin_amdgcn_readlane(rs, 31) +
-                  __builtin_amdgcn_readlane(rs, 47) + __builtin_amdgcn_readlane(rs, 63);
-  const int cge = cnt & 0xFFFF, cle = (int)((uint32_t)cnt >> 16);  // <= 64 * JM each
-  int ge_before = 0, le_before = 0, tot_le = cle;
+  KVC_TICK(tb);
+  int ge_before = 0, le_before = 0, tot_le = cle, tot_ge = cge;
   if constexpr (NW > 1) {
     static_assert(NW <= 16, "cross-wave scans use one 16-lane DPP row");
     if (lane == 0)  // sums < 2^16 (positions < 65536): packed
       sc.wa[wid] = (int)((uint32_t)cge | ((uint32_t)cle << 16));
+    KVC_TICK(tc);
     __syncthreads();  // B_a
     const int scan = row_scan16(lane < NW ? sc.wa[lane] : 0);
     // unpack unsigned: the le half reaches bit 31 for segments longer than 32767 positions
     const uint32_t before = wid ? (uint32_t)__builtin_amdgcn_readlane(scan, wid - 1) : 0u;
     ge_before = (int)(before & 0xFFFFu);
     le_before = (int)(before >> 16);
-    tot_le = (int)((uint32_t)__builtin_amdgcn_readlane(scan, NW - 1) >> 16);
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane(scan, NW - 1);
+    tot_le = (int)(tot >> 16);
+    tot_ge = (int)(tot & 0xFFFFu);
   }
   KVC_TICK(t1);
-  // ---- P2: s rank table, swap count m, g_{m+1} (stores only).  The tables hold the ranks
-  // (wb, wb + cap] of one window: window 0 also counts m; a level with m > cap re-scatters the
-  // next window from its flags (still in registers; the swapped pairs are disjoint, so earlier
-  // windows' swaps do not change them) after the previous window's swaps ----
-  if (tid == 0) kv_swap(key, idx, lo, ch);  // the median move, made physical
-  int msw = 0, gnext = kBig, wb = 0;
-  while (true) {
-    const bool count = wb == 0;
-    int rge = ge_before, rle = le_before, nsw = 0, ff = kBig;
-#pragma unroll
-    for (int j = 0; j < JM; ++j) {
-      if (j >= J) break;
+  // ---- P2, rank window 0: s / g rank tables, swap count m, g_{m+1} (stores only) ----
+  int nsw = 0;
+  if (whole && !owner)
+    p2_window0<KeyT, JM, true>(key, spos, gpos, lane, pos0, wbeg, J, hi, p, ch, kge, kle,
+                               ge_before + 1, le_before, tot_le, cap, nsw);
+  else if (nval > 0)
+    p2_window0<KeyT, JM, false>(key, spos, gpos, lane, pos0, wbeg, J, hi, p, ch, kge, kle,
+                                ge_before + 1, le_before, tot_le, cap, nsw);
+  // the median move, made physical by the only wave that reads slot ch (after its P2 loads)
+  if (owner && lane == 0) kv_swap(key, idx, lo, ch);
+  int msw;
+  if constexpr (NW > 1) {
+    if (lane == 0) sc.wm[wid] = nsw;
+    __syncthreads();  // B_b
+    msw = __builtin_amdgcn_readlane(row_scan16(lane < NW ? sc.wm[lane] : 0), NW - 1);
+  } else {
+    wave_sync();
+    msw = nsw;
+  }
+  // g_{m+1}, the first unswapped ge position (none when every ge position is swapped)
+  int gnext = msw >= tot_ge ? kBig : msw < cap ? uni((int)gpos[msw + 1]) : kBig;
+  KVC_TICK(t2);
+  // ---- m >= cap (rare): the level's flags, from the keys before any swap (the median slot is
+  // physical now), kept in registers for the later windows' scatters (the swapped pairs are
+  // disjoint, so earlier windows' swaps do not change them), and g_{m+1} from a flag pass ----
+  MaskT gem = 0, lem = 0;
+  if (msw >= cap) {
+    for (int j = 0; j < J; ++j) {
+      const int pos = pos0 + j * 64;
+      const bool inb = pos < hi;
+      const uint32_t kk = (uint32_t)key[min(pos, hi - 1)];
+      gem |= (inb && kk >= p) ? ((MaskT)1 << j) : (MaskT)0;
+      lem |= (inb && kk <= p) ? ((MaskT)1 << j) : (MaskT)0;
+    }
+    int rge = ge_before, rle = le_before, ff = kBig;
+    for (int j = 0; j < J && ff == kBig; ++j) {
       const bool ge = (gem >> j) & 1, le = (lem >> j) & 1;
       const uint64_t bg = __builtin_amdgcn_ballot_w64(ge), bl = __builtin_amdgcn_ballot_w64(le);
-      const int A = mbcnt(bg, rge);                 // ge positions before this one
-      const int lin = mbcnt(bl, rle) + (le ? 1 : 0);  // le positions in [lo+1, pos]
-      const bool cond = A + lin < tot_le;
-      const uint16_t pj = (uint16_t)(pos0 + j * 64);
-      const int sr = tot_le - lin + 1 - wb;  // s rank within the window
-      spos[(le && sr >= 1 && sr <= cap) ? sr : lane - 64] = pj;
-      const int gr = A + 1 - wb;             // swapped (cond): g rank A + 1 <= m
-      gpos[(ge && cond && gr >= 1 && gr <= cap) ? gr : lane - 64] = pj;
-      if (count) {
-        const uint64_t bc = __builtin_amdgcn_ballot_w64(cond);
-        nsw += __popcll(bg & bc);
-        const uint64_t bf = bg & ~bc;  // first unswapped ge: positions grow with j, so min = first
-        ff = min(ff, bf ? wbeg + j * 64 + (int)__builtin_ctzll(bf) : kBig);
-      }
+      const bool cond = mbcnt(bg, rge) + mbcnt(bl, rle) + (le ? 1 : 0) < tot_le;
+      const uint64_t bf = bg & ~__builtin_amdgcn_ballot_w64(cond);
+      if (bf) ff = wbeg + j * 64 + (int)__builtin_ctzll(bf);
       rge += __popcll(bg);
       rle += __popcll(bl);
     }
-    if (count) {
-      if constexpr (NW > 1) {
-        if (lane == 0)  // ff < 65535
-          sc.wm[wid] = (int)((uint32_t)nsw | ((uint32_t)(ff == kBig ? 0xFFFF : ff) << 16));
-        __syncthreads();  // B_b
-        const uint32_t x = lane < NW ? (uint32_t)sc.wm[lane] : 0xFFFF0000u;
-        msw = __builtin_amdgcn_readlane(row_scan16((int)(x & 0xFFFFu)), NW - 1);
-        // waves in position order: the first one with an unswapped ge position wins
-        const uint64_t fb = __builtin_amdgcn_ballot_w64((x >> 16) != 0xFFFFu);
-        gnext = fb ? (int)((uint32_t)__builtin_amdgcn_readlane((int)x, (int)__builtin_ctzll(fb)) >> 16)
-                   : kBig;
-      } else {
-        wave_sync();
-        msw = nsw;
-        gnext = ff;
-      }
-      KVC_TICK(t2);
+    if constexpr (NW > 1) {
+      if (lane == 0) sc.wb[wid] = ff == kBig ? 0xFFFF : ff;  // ff < 65535
+      __syncthreads();  // every wave has its flags before the first swap
+      const uint32_t x = lane < NW ? (uint32_t)sc.wb[lane] : 0xFFFFu;
+      // waves in position order: the first one with an unswapped ge position wins
+      const uint64_t fb = __builtin_amdgcn_ballot_w64(x != 0xFFFFu);
+      gnext = fb ? __builtin_amdgcn_readlane((int)x, (int)__builtin_ctzll(fb)) : kBig;
     } else {
-      group_sync<NT>();
+      wave_sync();
+      gnext = ff;
     }
+  }
+  int wb = 0;
+  while (true) {
     // ---- P4: this window's swaps (disjoint pairs g_t <-> s_t), spread evenly over the NT
     // lanes: rank-table loads, then key/idx loads, then stores ----
     const int wend = min(msw, wb + cap);
@@ -823,6 +915,23 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
     if (wend >= msw) break;
     group_sync<NT>();  // the next window overwrites the tables
     wb += cap;
+    // ---- scatter of window wb from the flags (ranks (wb, wb + cap]) ----
+    int rge = ge_before, rle = le_before;
+    for (int j = 0; j < J; ++j) {
+      const bool ge = (gem >> j) & 1, le = (lem >> j) & 1;
+      const uint64_t bg = __builtin_amdgcn_ballot_w64(ge), bl = __builtin_amdgcn_ballot_w64(le);
+      const int A = mbcnt(bg, rge);                   // ge positions before this one
+      const int lin = mbcnt(bl, rle) + (le ? 1 : 0);  // le positions in [lo+1, pos]
+      const bool cond = A + lin < tot_le;
+      const uint16_t pj = (uint16_t)(pos0 + j * 64);
+      const int sr = tot_le - lin + 1 - wb;  // s rank within the window
+      spos[(le && sr >= 1 && sr <= cap) ? sr : lane - 64] = pj;
+      const int gr = A + 1 - wb;             // swapped (cond): g rank A + 1 <= m
+      gpos[(ge && cond && gr >= 1 && gr <= cap) ? gr : lane - 64] = pj;
+      rge += __popcll(bg);
+      rle += __popcll(bl);
+    }
+    group_sync<NT>();
   }
   group_sync<NT>();  // B_c
   KVC_TICK(t3);
@@ -834,6 +943,12 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
     acc[3] += 1;
     acc[4] += (uint64_t)msw;
     if (NT > 64) acc[25] = (t1 - t0) | ((t2 - t1) << 20) | ((t3 - t2) << 40);  // level split
+    if (NT > 64 && JM == 16 && J == 16) {  // level 0 of a 16 384-position row (slots 26..29)
+      acc[21] = ta - t0;
+      acc[22] = tb - ta;
+      acc[23] = tc - tb;
+      acc[24] = t1 - tc;
+    }
   }
 #endif
   return min(gnext, msw > 0 ? uni((int)spos[msw - wb]) : kBig);
@@ -855,7 +970,7 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
 // global-memory variant of zones longer than kZoneMax).
 // Returns 0 when the first-k set is final, 1 when the block hands a short segment to one wave.
 template <typename KeyT, int NT, int MAXJ>
-__device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, uint16_t* gpos,
+__device__ __forceinline__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, uint16_t* gpos,
                          SelScalars<KeyT>& sc, int k, bool topk, int thr, int cap, int& lo,
                          int& hi, int& depth, int& level, int wave_seg,
                          uint64_t* acc = nullptr) {
@@ -910,11 +1025,13 @@ __device__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, uint16_t* gpo
       acc[12 + 2 * level] = acc[25];  // P1 | P2 << 20 | P4 << 40 of this level
     }
 #endif
-    if (topk) {  // std::__introselect: if (cut <= nth) first = cut; else last = cut;
-      if (cut <= k - 1) lo = cut; else hi = cut;
-    } else {     // std::__introsort_loop: recurse right, loop on the left part
-      if (k <= cut) hi = cut; else lo = cut;
-    }
+    // std::__introselect: if (cut <= nth) first = cut; else last = cut;
+    // std::__introsort_loop: recurse right, loop on the left part (k <= cut: keep the left).
+    // Value selects, not branches: a store through a selected pointer to lo / hi would put
+    // them in scratch memory.
+    const bool right = topk ? cut <= k - 1 : k > cut;
+    lo = right ? cut : lo;
+    hi = right ? hi : cut;
     ++level;
   }
 }
