@@ -810,6 +810,12 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
     if (lane == 0)  // sums < 2^16 (positions < 65536): packed
       sc.wa[wid] = (int)((uint32_t)cge | ((uint32_t)cle << 16));
     KVC_TICK(tc);
+#ifdef KVC_STAMPS
+    if (lane == 0) {  // diagnostic: this wave's level start and P1 end (low 32 bits)
+      sc.wb[wid] = (int)(uint32_t)t0;
+      sc.fnan[wid] = (int)(uint32_t)tc;
+    }
+#endif
     __syncthreads();  // B_a
     const int scan = row_scan16(lane < NW ? sc.wa[lane] : 0);
     // unpack unsigned: the le half reaches bit 31 for segments longer than 32767 positions
@@ -832,6 +838,20 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
   // the median move, made physical by the only wave that reads slot ch (after its P2 loads)
   if (owner && lane == 0) kv_swap(key, idx, lo, ch);
   int msw;
+#ifdef KVC_STAMPS
+  uint64_t tp2 = 0;
+  KVC_TICK(tp2);
+  uint32_t wstart[NW > 1 ? NW : 1], wp1[NW > 1 ? NW : 1];
+  if constexpr (NW > 1) {
+    if (acc && tid == 0 && JM == 16 && J == 16)
+      for (int w = 0; w < NW; ++w) {
+        wstart[w] = (uint32_t)sc.wb[w];
+        wp1[w] = (uint32_t)sc.fnan[w];
+      }
+    __syncthreads();  // diagnostic: the P1 stamps are read before P2 stamps overwrite them
+    if (lane == 0) sc.fnan[wid] = (int)(uint32_t)tp2;
+  }
+#endif
   if constexpr (NW > 1) {
     if (lane == 0) sc.wm[wid] = nsw;
     __syncthreads();  // B_b
@@ -943,11 +963,23 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
     acc[3] += 1;
     acc[4] += (uint64_t)msw;
     if (NT > 64) acc[25] = (t1 - t0) | ((t2 - t1) << 20) | ((t3 - t2) << 40);  // level split
-    if (NT > 64 && JM == 16 && J == 16) {  // level 0 of a 16 384-position row (slots 26..29)
-      acc[21] = ta - t0;
-      acc[22] = tb - ta;
-      acc[23] = tc - tb;
-      acc[24] = t1 - tc;
+    if (NT > 64 && JM == 16 && J == 16) {  // level 0 of a 16 384-position row (slots 26..29):
+      // wave start skew, longest wave P1 (start -> counts written), last P1 end after the first
+      // start, last P2 end after B_a (wave 0's t1)
+      uint32_t s0 = wstart[0], s1 = wstart[0], p1m = 0, e1 = 0, e2 = 0;
+      for (int w = 0; w < NW; ++w) {
+        s0 = min(s0, wstart[w]);
+        s1 = max(s1, wstart[w]);
+      }
+      for (int w = 0; w < NW; ++w) {
+        p1m = max(p1m, wp1[w] - wstart[w]);
+        e1 = max(e1, wp1[w] - s0);
+        e2 = max(e2, (uint32_t)sc.fnan[w] - (uint32_t)t1);
+      }
+      acc[21] = s1 - s0;
+      acc[22] = p1m;
+      acc[23] = e1;
+      acc[24] = e2;
     }
   }
 #endif
@@ -1152,6 +1184,27 @@ __device__ bool select_fast_untied(const KeyT* key, int n, int k, SelScalars<Key
 // global scratch row for zones longer than kZoneMax) and scalars in `sc`; NT threads (the
 // workgroup) cooperate.  Emits the kept zone-local indices in ascending order to `out` (global
 // int32) or, with TO_LDS, to `sel` (LDS u16, may alias the key region: keys are dead by then).
+// Exclusive prefix sum of one int per thread over the NT threads of the block (wave scans as
+// four 16-lane DPP row scans, wave totals through `buf`); one barrier.
+template <int NT>
+__device__ __forceinline__ int block_exclusive_scan(int v, int* buf, int lane, int wid) {
+  static_assert(NT / 64 <= 16, "one 16-lane DPP row holds the wave totals");
+  const int rs = row_scan16(v);  // inclusive within each 16-lane row
+  const int r0 = __builtin_amdgcn_readlane(rs, 15), r1 = __builtin_amdgcn_readlane(rs, 31);
+  const int r2 = __builtin_amdgcn_readlane(rs, 47), r3 = __builtin_amdgcn_readlane(rs, 63);
+  const int row = lane >> 4;
+  const int excl = rs - v + (row > 0 ? r0 : 0) + (row > 1 ? r1 : 0) + (row > 2 ? r2 : 0);
+  if constexpr (NT == 64) {
+    return excl;
+  } else {
+    if (lane == 0) buf[wid] = r0 + r1 + r2 + r3;
+    __syncthreads();
+    const int ws = row_scan16(lane < NT / 64 ? buf[lane] : 0);
+    const int w = uni(wid);
+    return excl + (w ? __builtin_amdgcn_readlane(ws, w - 1) : 0);
+  }
+}
+
 template <int KC, bool TO_LDS, int MAXN, int NT>
 __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, int dt, int order,
                             int algo, const char* __restrict__ nrow, int32_t* out, uint16_t* sel,
@@ -1284,44 +1337,37 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
   __syncthreads();
   KVC_STAMP(3);
 
-  // ---- emit the kept set {idx[0..k)} as ascending zone-local indices (flags in the key
-  // region: the keys are dead, and every flag is read into registers before `sel` is written)
-  uint16_t* flag = reinterpret_cast<uint16_t*>(key);
-  for (int i = tid; i < n; i += NT) flag[i] = 0;
+  // ---- emit the kept set {idx[0..k)} as ascending zone-local indices: a bitmap of the kept
+  // positions over the (dead) key region, one block scan of per-thread popcounts, and each
+  // thread writing the positions of its words.  Every bitmap word is in registers before the
+  // scan's barrier, so `sel` (which aliases the key region) is only written after it.
+  uint32_t* bm = reinterpret_cast<uint32_t*>(key);
+  const int nw = (n + 31) >> 5;
+  for (int w = tid; w < nw; w += NT) bm[w] = 0u;
   __syncthreads();
-  for (int i = tid; i < k; i += NT) flag[idx[i]] = 1;
-  __syncthreads();
-  const int J = (n + NT - 1) / NT;
-  const int wbeg = wid * J * 64;
-  uint64_t fm = 0;  // J <= 64
-  int cl = 0;       // per-lane count: no scalar popcount waits on a ballot inside the loop
-  for (int j = 0; j < J; ++j) {
-    const int pos = wbeg + j * 64 + lane;
-    const bool f = pos < n && flag[pos] != 0;
-    fm |= (uint64_t)f << j;
-    cl += f ? 1 : 0;
-  }
-  {
-    const int rs = row_scan16(cl);
-    const int c = __builtin_amdgcn_readlane(rs, 15) + __builtin_amdgcn_readlane(rs, 31) +
-                  __builtin_amdgcn_readlane(rs, 47) + __builtin_amdgcn_readlane(rs, 63);
-    if (lane == 0) sc.wa[wid] = c;
+  for (int i = tid; i < k; i += NT) {
+    const int x = idx[i];
+    atomicOr(&bm[x >> 5], 1u << (x & 31));
   }
   __syncthreads();
-  int run = 0;  // kept positions in the waves before this one
-  if constexpr (NT > 64) {
-    const int ws = row_scan16(lane < NT / 64 ? sc.wa[lane] : 0);
-    run = wid ? __builtin_amdgcn_readlane(ws, wid - 1) : 0;
+  constexpr int MAXW = (MAXN / 32 + NT - 1) / NT;  // bitmap words per thread
+  uint32_t wv[MAXW];
+  int cnt = 0;
+#pragma unroll
+  for (int q = 0; q < MAXW; ++q) {
+    const int w = tid * MAXW + q;
+    wv[q] = w < nw ? bm[w] : 0u;
+    cnt += __popc(wv[q]);
   }
-  for (int j = 0; j < J; ++j) {
-    const bool f = (fm >> j) & 1;
-    const uint64_t bf = __ballot(f);
-    if (f) {
-      const int r = mbcnt(bf, run);
-      if constexpr (TO_LDS) sel[r] = (uint16_t)(wbeg + j * 64 + lane);
-      else out[r] = wbeg + j * 64 + lane;
+  int r = block_exclusive_scan<NT>(cnt, sc.wa, lane, wid);
+#pragma unroll
+  for (int q = 0; q < MAXW; ++q) {
+    const int base = (tid * MAXW + q) * 32;
+    for (uint32_t b = wv[q]; b; b &= b - 1u, ++r) {
+      const int pos = base + (int)__builtin_ctz(b);
+      if constexpr (TO_LDS) sel[r] = (uint16_t)pos;
+      else out[r] = pos;
     }
-    run += vpopc(bf);
   }
   KVC_STAMP(4);
 }

@@ -75,7 +75,8 @@ if os.environ.get("SEL_P1_STAMPS"):  # diagnostic: level-0 P1 sub-phases (slots 
     ph = allst[:, 26:30].astype(np.float64)
     print(json.dumps({"level0_P1_phases_median": {
         n: float(np.median(ph[:, i])) for i, n in enumerate(
-            ("median_of_3", "key_loads_and_flags", "wave_counts", "barrier_B_a"))}}))
+            ("wave_start_skew", "longest_wave_P1", "last_P1_end_after_first_start",
+             "last_P2_end_after_B_a"))}}))
 if os.environ.get("SEL_SNAP_STAMPS"):  # diagnostic: snapkv scoring phases (slots 26..29)
     sn = allst[:, [1 - 1 + 1, 26, 27, 28, 29]]
     ph = np.stack([allst[:, 26] - allst[:, 0], allst[:, 27] - allst[:, 26],
