@@ -283,9 +283,10 @@ def _params(dtype, B, H, D, order, algo, external):
 
 
 def _outputs(device, dtype, B, H, D, n_outs):
-    """Fresh contiguous [B,H,n_out,D] K and V per layer, and their data pointers.  Layers of one
-    output length share one allocation (decode steps: 64 tensors per token); each layer's K / V
-    is a disjoint contiguous view of it ("Output tensors")."""
+    """Fresh contiguous [B,H,n_out,D] K and V per layer, and their data pointers.  All outputs
+    of a call share one allocation (decode steps: 64 tensors per token; one torch.empty per
+    tensor was most of pyramid_kv's host time); each layer's K / V is a disjoint contiguous view
+    of it ("Output tensors")."""
     n = len(n_outs)
     if all(x == n_outs[0] for x in n_outs):
         buf = torch.empty((2 * n, B, H, n_outs[0], D), dtype=dtype, device=device)
@@ -293,9 +294,14 @@ def _outputs(device, dtype, B, H, D, n_outs):
         step = B * H * n_outs[0] * D * _ESIZE[dtype]
         offs = np.arange(2 * n, dtype=np.uint64) * np.uint64(step) + np.uint64(buf.data_ptr())
         return o[:n], o[n:], offs[:n], offs[n:]
-    kos = [torch.empty((B, H, x, D), dtype=dtype, device=device) for x in n_outs]
-    vos = [torch.empty((B, H, x, D), dtype=dtype, device=device) for x in n_outs]
-    return kos, vos, [t.data_ptr() for t in kos], [t.data_ptr() for t in vos]
+    sizes = [B * H * x * D for x in n_outs] * 2  # K outputs, then V outputs
+    buf = torch.empty(sum(sizes), dtype=dtype, device=device)
+    parts = buf.split(sizes)
+    shapes = [(B, H, x, D) for x in n_outs] * 2
+    o = [t.view(s) for t, s in zip(parts, shapes)]
+    offs = np.concatenate(([0], np.cumsum(sizes[:-1]))).astype(np.uint64)
+    offs = offs * np.uint64(_ESIZE[dtype]) + np.uint64(buf.data_ptr())
+    return o[:n], o[n:], offs[:n], offs[n:]
 
 
 def _run_plain(device, dtype, B, H, D, kps, vps, segs, js, out_list, order, algo):

@@ -242,6 +242,32 @@ def test_repeated_call_shapes_reuse_plan_safely():
                 assert np.array_equal(to_np(ko), rk) and np.array_equal(to_np(vo), rv)
 
 
+def test_variable_size_outputs_are_disjoint_views():
+    """pyramid_kv gives every layer its own n_out; the engine carves all K/V outputs out of one
+    allocation (INTEGRATION.md "Output tensors"): each output is contiguous with its own shape,
+    no two overlap, writing one leaves the others intact, and the values match the oracle."""
+    from kvcompress.methods import pyramid_kv_compress
+    layers_np = [(prng.gen_keys(900 + i, (1, 4, 700, 64), "bf16"),
+                  prng.gen_values(900 + i, (1, 4, 700, 64), "bf16")) for i in range(6)]
+    kw = dict(base_size=400, min_size=64, profile="linear", skip_layers=[])
+    out = pyramid_kv_compress([(to_dev(k), to_dev(v)) for k, v in layers_np], **kw)
+    ref = oracle.pyramid_kv_compress(layers_np, **kw)
+    torch.cuda.synchronize()
+    spans = []
+    for (ko, vo), (rk, rv, _) in zip(out, ref):
+        assert np.array_equal(to_np(ko), rk) and np.array_equal(to_np(vo), rv)
+        for t in (ko, vo):
+            assert t.is_contiguous() and t.data_ptr() % 16 == 0
+            spans.append((t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()))
+    assert len({k.shape[2] for k, _ in out}) > 1  # the layers really differ in size
+    spans.sort()
+    assert all(a[1] <= b[0] for a, b in zip(spans, spans[1:]))
+    out[0][0].fill_(0)
+    for (ko, vo), (rk, rv, _) in list(zip(out, ref))[1:]:
+        assert np.array_equal(to_np(ko), rk) and np.array_equal(to_np(vo), rv)
+    assert np.array_equal(to_np(out[0][1]), ref[0][1])
+
+
 def test_no_cpu_fallback():
     from kvcompress.methods import fix_size_l2_compress
     K = torch.zeros(1, 2, 100, 64, dtype=torch.bfloat16)
