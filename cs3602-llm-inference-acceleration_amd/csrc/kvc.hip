@@ -963,7 +963,11 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
     acc[3] += 1;
     acc[4] += (uint64_t)msw;
     if (NT > 64) acc[25] = (t1 - t0) | ((t2 - t1) << 20) | ((t3 - t2) << 40);  // level split
+#ifdef KVC_SNAP_STAMPS
+    if (false) {  // slots 26..29 hold the snapkv scoring stamps (tools/gpu_snapstamps.sh)
+#else
     if (NT > 64 && JM == 16 && J == 16) {  // level 0 of a 16 384-position row (slots 26..29):
+#endif
       // wave start skew, longest wave P1 (start -> counts written), last P1 end after the first
       // start, last P2 end after B_a (wave 0's t1)
       uint32_t s0 = wstart[0], s1 = wstart[0], p1m = 0, e1 = 0, e2 = 0;
