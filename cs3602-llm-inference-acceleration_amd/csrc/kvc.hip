@@ -44,7 +44,7 @@ constexpr int kSmallZone = 4096;
 constexpr int kZoneMax = 16384;        // longest zone whose selection runs from LDS
 constexpr int kZoneMaxGlobal = 65536;  // longest zone of the u16-position global variant
 constexpr int kZoneMaxLong = 1 << 24;   // longest zone at all (u32 positions; global scratch)
-constexpr int kWaveSeg = 128;    // default: segments this short are finished by one wave
+constexpr int kWaveSeg = 256;  // segments this short are finished by one wave (64 / 128 / 512 / 1024 measured slower)
 constexpr int kGatherThreads = 256;
 constexpr int kGatherTokens = 64;  // output tokens per gather block
 constexpr int kBig = 0x7FFFFFFF;

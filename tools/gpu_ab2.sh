@@ -12,8 +12,8 @@ if [ "$1" != "notest" ]; then
 fi
 LIBDIR=cs3602-llm-inference-acceleration_amd/kvcompress/_lib
 : > $O/ab.jsonl
-run() {  # name method kw D
-  KVC_LIB=$LIBDIR/$lib AB_DTYPE=bf16 AB_S=16384 AB_METHOD=$2 AB_KW="$3" AB_D=$4 \
+run() {  # name method kw D [S]
+  KVC_LIB=$LIBDIR/$lib AB_DTYPE=bf16 AB_S=${5:-16384} AB_METHOD=$2 AB_KW="$3" AB_D=$4 \
       timeout -k 10 180 python3 tools/phase_ab.py > $O/one.json 2>$O/err || { tail $O/err; exit 1; }
   echo "{\"rep\": $rep, \"case\": \"$1\", \"r\": $(cat $O/one.json)}" >> $O/ab.jsonl
 }
@@ -24,6 +24,7 @@ for rep in 1 2; do
     run pyramid pyramid_kv '{}' 128 || exit 1
     run snapkv512 snapkv_lite '{"keep_size": 512}' 128 || exit 1
     run fix512_kr05 fix_size_l2 '{"fix_kv_size": 512, "keep_ratio": 0.5}' 128 || exit 1
+    run fix512_s4096 fix_size_l2 '{"fix_kv_size": 512}' 128 4096 || exit 1
   done
 done
 python3 - <<'PY'
