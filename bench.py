@@ -97,7 +97,7 @@ def job_bytes(jobs, es):
     return {"path": path, "score": score, "select+gather": gather}
 
 
-PMC_FILE = "profiles/r02_i_pmc_traffic.json"  # tools/pmc_round.sh (tools/gpu_final.sh) + tools/pmc_traffic.py
+PMC_FILE = "profiles/r02_i_pmc_traffic.json"  # tools/pmc_round.sh (tools/gpu.sh pmc) + tools/pmc_traffic.py
 
 
 def pmc_traffic(kernel="kvc::score_kernel<1, 16, true>"):
@@ -251,8 +251,8 @@ def timed_steps(step, steps, warmup, dist, sync, device, on_start=None):
     sync()
     elapsed = time.perf_counter() - t0
     del out
-    if dist:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    if dist:  # gloo on a host tensor: the harness needs no device collective
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed
@@ -351,11 +351,10 @@ def main():
         sync = torch.cuda.synchronize
     dist = None
     if world > 1:
+        # gloo on host tensors: the only cross-rank operations are the timing barrier and two
+        # MAX / SUM all-reduces of host scalars -- the data path has no exchange, so no RCCL
         import torch.distributed as dist
-        if args.dry_run:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=dev)
+        dist.init_process_group("gloo")
 
     from kvcompress import _engine
     from kvcompress.methods import get_compress_fn
@@ -401,15 +400,15 @@ def main():
 
         es = layers[0][0].element_size() if layers else 2
         nbytes = job_bytes(capture_jobs(step), es)
-        # per-kernel durations: the engine splits each launch into its kernels with HIP events
-        # (recorded on the stream they run on) for the whole timed region.  The events are
-        # created with hipEventDisableSystemFence: recording torch's default events between the
-        # kernels writes back / invalidates caches and cost the step 1.5-2.3 %, these ~1 %
-        # (tools/timer_overhead.py, profiles/r02_timer_overhead.json)
+        # per-kernel durations come from a SECOND pass of K steps after the timed one: the engine
+        # then splits each launch into its kernels with HIP events recorded on the stream they
+        # run on (created with hipEventDisableSystemFence).  The timed pass itself runs exactly
+        # the untimed call (no events, no split launches).
         timer = _engine.PhaseTimer(fenceless=True)
-    elapsed = timed_steps(step, args.steps, args.warmup, dist, sync, dev,
-                          on_start=(lambda: _engine.set_phase_timer(timer)) if timer else None)
+    elapsed = timed_steps(step, args.steps, args.warmup, dist, sync, dev)
     if timer:
+        _engine.set_phase_timer(timer)
+        timed_steps(step, args.steps, 0, dist, sync, dev)
         _engine.set_phase_timer(None)
         dur = {k: sum(v) / len(v) for k, v in timer.durations_ms().items()}
     else:
@@ -418,7 +417,6 @@ def main():
     # units all ranks processed: positions scored (layers x S) per step
     units = torch.tensor([n_layers * seq_len], dtype=torch.float64)
     if dist:
-        units = units.to(dev)
         dist.all_reduce(units)
     units = float(units.item())
 

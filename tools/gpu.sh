@@ -1,0 +1,81 @@
+#!/bin/bash
+# One GPU-box runner for every measurement this repo takes (replaces the round-1/2 one-off
+# scripts).  Usage:  bash tools/gpu.sh STEP [STEP ...]   with STEP one of
+#   test       pytest -m gpu (the driver's parity tier)
+#   smoke      __graft_entry__.smoke()
+#   bench      python bench.py (headline, default K/W, CPU baseline + PPL leg)   -> bench.json
+#   quick      python bench.py --steps 20 --warmup 5 --no-cpu-baseline          -> quick.json
+#   trace      rocprofv3 --kernel-trace --stats of `bench.py --steps 20 --warmup 5`, plus the
+#              idle time between engine kernels (tools/trace_gaps.py)           -> prof/, gaps.json
+#   decode     per-token decode steps (tools/decode_bench.py)                   -> decode.json
+#   workloads  every bench.py workload at N=1                                   -> workloads.jsonl
+#   pmc        FETCH/WRITE traffic + SQ counters (tools/pmc_round.sh)
+#   ab         A/B of library builds named in $AB_LIBS (files in kvcompress/_lib) on the
+#              workloads in $AB_WORKLOADS (bench.py, 2 repeats)                   -> ab.jsonl
+# Every GPU step runs under its own time limit and the first failure ends the call.
+set -o pipefail
+R="${GRAFT_REPO_ROOT:-/root/repo}"
+O="$R/gpurun_out"
+LIBDIR="$R/cs3602-llm-inference-acceleration_amd/kvcompress/_lib"
+mkdir -p "$O"
+cd "$R"
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case "$step" in
+    test)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+          -p no:cacheprovider > "$O/pytest_gpu.log" 2>&1 || { tail -30 "$O/pytest_gpu.log"; exit 1; }
+      tail -2 "$O/pytest_gpu.log" ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 \
+          || { tail -20 "$O/smoke.log"; exit 1; }
+      grep smoke "$O/smoke.log" ;;
+    bench)
+      timeout -k 10 500 python bench.py > "$O/bench.json" 2> "$O/bench.err" || { tail "$O/bench.err"; exit 1; }
+      cat "$O/bench.json" ;;
+    quick)
+      timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$O/quick.json" \
+          2> "$O/quick.err" || { tail "$O/quick.err"; exit 1; }
+      cat "$O/quick.json" ;;
+    trace)
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+          --output-format csv -d "$O/prof" -o run -- python3 "$R/bench.py" --steps 20 --warmup 5 \
+          --no-cpu-baseline > "$O/prof.log" 2>&1 ) || { tail "$O/prof.log"; exit 1; }
+      python3 tools/trace_gaps.py "$(find "$O/prof" -name '*kernel_trace.csv' | head -1)" > "$O/gaps.json" \
+          && cat "$O/gaps.json" ;;
+    decode)
+      timeout -k 10 300 python tools/decode_bench.py > "$O/decode.json" 2> "$O/decode.err" \
+          || { tail "$O/decode.err"; exit 1; }
+      cat "$O/decode.json" ;;
+    workloads)
+      : > "$O/workloads.jsonl"
+      for w in ${WORKLOADS:-fix512-s16384 fix512-s4096 fix512-s4096-d80 streaming-s16384 h2o-s16384 snapkv-s16384 pyramid-s16384 l2-s16384 adaptive-s16384}; do
+        timeout -k 10 200 python bench.py --workload $w --steps 20 --warmup 5 --no-cpu-baseline \
+            >> "$O/workloads.jsonl" 2>> "$O/workloads.err" || { tail "$O/workloads.err"; exit 1; }
+      done
+      cat "$O/workloads.jsonl" ;;
+    pmc)
+      bash tools/pmc_round.sh > "$O/pmc_round.out" 2>&1 || { tail -20 "$O/pmc_round.out"; exit 1; }
+      tail -c 3000 "$O/pmc_round.out" ;;
+    ab)
+      : > "$O/ab.jsonl"
+      for rep in 1 2; do
+        for lib in ${AB_LIBS:?}; do
+          for w in ${AB_WORKLOADS:-fix512-s16384}; do
+            KVC_LIB="$LIBDIR/$lib" timeout -k 10 200 python bench.py --workload $w --steps 20 \
+                --warmup 5 --no-cpu-baseline > "$O/ab_one.json" 2> "$O/ab.err" || { tail "$O/ab.err"; exit 1; }
+            echo "{\"rep\": $rep, \"lib\": \"$lib\", \"workload\": \"$w\", \"r\": $(cat "$O/ab_one.json")}" >> "$O/ab.jsonl"
+          done
+        done
+      done
+      python3 - "$O/ab.jsonl" <<'EOF'
+import json, sys
+for l in open(sys.argv[1]):
+    d = json.loads(l); r = d["r"]
+    print(d["rep"], d["lib"], d["workload"], round(r["ms_per_step"], 4),
+          {k: round(v, 4) for k, v in r["kernel_ms_per_step"].items()})
+EOF
+      ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done

@@ -1,5 +1,5 @@
 """Per-launch HBM traffic of the engine kernels from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE
-passes (tools/gpu_check.sh pmc) -> profiles/<name>_pmc_traffic.json.
+passes (tools/gpu.sh pmc) -> profiles/<name>_pmc_traffic.json.
 
 FETCH_SIZE / WRITE_SIZE are KiB.  On gfx950 FETCH_SIZE sees only half of wide coalesced read
 streams (MI355X_MICROARCH.md, HBM / rocprofv3 section), so FETCH x2 is the HBM read estimate.
