@@ -1209,12 +1209,14 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int* buf, int lane, i
   }
 }
 
+// Returns false (and ORs KVC_DEV_SELECT_BOUNDS into *status) when the row exceeds this kernel's
+// zone capacity -- nothing is selected then.
 template <int KC, bool TO_LDS, int MAXN, int NT>
-__device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, int dt, int order,
+__device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, int dt, int order,
                             int algo, const char* __restrict__ nrow, int32_t* out, uint16_t* sel,
                             char* arrays, int n_cap, int cap,
                             SelScalars<typename DTypeTraits<KC>::key_t>& sc,
-                            int wave_seg, uint64_t* stamps) {
+                            int wave_seg, uint64_t* stamps, uint32_t* status) {
   typedef typename DTypeTraits<KC>::key_t KeyT;
   constexpr int ESZ = DTypeTraits<KC>::esz;
   constexpr int MAXJ = (MAXN + NT - 1) / NT;  // positions per lane, level 0
@@ -1225,14 +1227,18 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
   KVC_STAMP(0);
   const int n = ly->zone_len;
   const int k = ly->n_select;
-  if (k <= 0 || n <= 0 || n > MAXN || n > n_cap) return;
+  if (n > MAXN || n > n_cap) {  // a dispatch bug, never silent: flag it, select nothing
+    if (threadIdx.x == 0 && status) atomicOr(status, (uint32_t)KVC_DEV_SELECT_BOUNDS);
+    return false;
+  }
+  if (k <= 0 || n <= 0) return true;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (k >= n) {  // keep everything (e.g. h2o_l2 when the middle is no longer than heavy_hitter)
     for (int i = tid; i < n; i += NT) {
       if constexpr (TO_LDS) sel[i] = (uint16_t)i;
       else out[i] = i;
     }
-    return;
+    return true;
   }
   const bool desc = order == KVC_DESC;
 
@@ -1311,7 +1317,7 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
     // (`sel` may alias the key region: the keys are read into registers before any store)
     if (select_fast_untied<NT, MAXJ, KeyT, TO_LDS>(key, n, k, sc, out, sel)) {
       KVC_STAMP(31);  // diagnostic build: fast path taken
-      return;
+      return true;
     }
   }
   const bool topk = algo == KVC_ALGO_TOPK;
@@ -1374,6 +1380,7 @@ __device__ __forceinline__ void select_body(const kvc_layer_t* __restrict__ ly, 
     }
   }
   KVC_STAMP(4);
+  return true;
 }
 
 
@@ -1391,7 +1398,7 @@ __global__ void __launch_bounds__(NT, 8)  // 8 waves per SIMD: two 1024-thread r
     select_kernel(const LayerChunk T, int BH, int dt, int order, int algo,
                   const char* __restrict__ norms, int64_t norm_stride,
                   int32_t* __restrict__ out_idx, int64_t idx_stride, int wave_seg, int n_cap,
-                  int cap, uint64_t* stamps) {
+                  int cap, uint64_t* stamps, uint32_t* status) {
   typedef typename DTypeTraits<KC>::key_t KeyT;
   constexpr int ESZ = DTypeTraits<KC>::esz;
   constexpr int MAXN = NT == kSelThreads ? kZoneMax : NT * 16;
@@ -1404,13 +1411,13 @@ __global__ void __launch_bounds__(NT, 8)  // 8 waves per SIMD: two 1024-thread r
     select_body<KC, false, MAXN, NT>(ly, dt, order, algo,
                                      norms + (int64_t)row * norm_stride * ESZ,
                                      out_idx + (int64_t)row * idx_stride, nullptr, smem, kZoneMax,
-                                     kSelCapBig<KeyT>, sc, wave_seg, stamps);
+                                     kSelCapBig<KeyT>, sc, wave_seg, stamps, status);
   } else {
     extern __shared__ __attribute__((aligned(16))) char dsmem[];
     select_body<KC, false, MAXN, NT>(ly, dt, order, algo,
                                      norms + (int64_t)row * norm_stride * ESZ,
                                      out_idx + (int64_t)row * idx_stride, nullptr, dsmem, n_cap,
-                                     cap, sc, wave_seg, stamps);
+                                     cap, sc, wave_seg, stamps, status);
   }
 }
 
@@ -1422,7 +1429,8 @@ __global__ void __launch_bounds__(kSelThreads)
     select_global_kernel(const LayerChunk T, int BH, int dt, int order, int algo,
                          const char* __restrict__ norms, int64_t norm_stride,
                          int32_t* __restrict__ out_idx, int64_t idx_stride, int wave_seg,
-                         char* __restrict__ scratch, int64_t scratch_row_bytes, int n_cap) {
+                         char* __restrict__ scratch, int64_t scratch_row_bytes, int n_cap,
+                         uint32_t* status) {
   typedef typename DTypeTraits<KC>::key_t KeyT;
   constexpr int ESZ = DTypeTraits<KC>::esz;
   __shared__ SelScalars<KeyT> sc;
@@ -1431,7 +1439,7 @@ __global__ void __launch_bounds__(kSelThreads)
   select_body<KC, false, kZoneMaxGlobal, kSelThreads>(
       ly, dt, order, algo, norms + (int64_t)row * norm_stride * ESZ,
       out_idx + (int64_t)row * idx_stride, nullptr, scratch + (int64_t)row * scratch_row_bytes,
-      n_cap, n_cap / 2 + 1, sc, wave_seg, nullptr);
+      n_cap, n_cap / 2 + 1, sc, wave_seg, nullptr, status);
 }
 
 // Zones longer than kZoneMaxGlobal (up to kZoneMaxLong): the same partition chain with u32
@@ -1547,7 +1555,8 @@ __global__ void __launch_bounds__(kSelThreads)
     select_long_kernel(const LayerChunk T, int BH, int dt, int order, int algo,
                        const char* __restrict__ norms, int64_t norm_stride,
                        int32_t* __restrict__ out_idx, int64_t idx_stride,
-                       char* __restrict__ scratch, int64_t scratch_row_bytes, int n_cap) {
+                       char* __restrict__ scratch, int64_t scratch_row_bytes, int n_cap,
+                       uint32_t* status) {
   typedef typename DTypeTraits<KC>::key_t KeyT;
   constexpr int ESZ = DTypeTraits<KC>::esz;
   __shared__ SelScalars<KeyT> ssc;
@@ -1555,7 +1564,11 @@ __global__ void __launch_bounds__(kSelThreads)
   const kvc_layer_t* ly = T.l + blockIdx.x / BH;
   const int row = ly->row0 + (int)(blockIdx.x % BH);
   const int n = ly->zone_len, k = ly->n_select;
-  if (k <= 0 || n <= 0 || n > n_cap || n > kZoneMaxLong) return;
+  if (n > n_cap || n > kZoneMaxLong) {
+    if (threadIdx.x == 0 && status) atomicOr(status, (uint32_t)KVC_DEV_SELECT_BOUNDS);
+    return;
+  }
+  if (k <= 0 || n <= 0) return;
   const char* nrow = norms + (int64_t)row * norm_stride * ESZ;
   int32_t* out = out_idx + (int64_t)row * idx_stride;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1651,7 +1664,8 @@ __global__ void __launch_bounds__(kSelThreads)
 template <int DT, int NC, bool NTS>
 __global__ void __launch_bounds__(kGatherThreads)
     gather_kernel(const LayerChunk T, int H, int BH,
-                  const int32_t* __restrict__ gidx, int64_t idx_stride) {
+                  const int32_t* __restrict__ gidx, int64_t idx_stride, int shared,
+                  uint32_t* status) {
   const kvc_layer_t* L = T.l;
   // grid = (rows, output-token blocks); one block copies kGatherTokens output rows of K and V
   constexpr int ESZ = DTypeTraits<DT>::esz;
@@ -1670,7 +1684,8 @@ __global__ void __launch_bounds__(kGatherThreads)
   const char* vb = static_cast<const char*>(ly->v) +
                    ((int64_t)b * ly->v_stride[0] + (int64_t)h * ly->v_stride[1]) * ESZ;
   const int64_t kss = ly->k_stride[2] * ESZ, vss = ly->v_stride[2] * ESZ;
-  const int32_t* irow = gidx + (int64_t)(ly->row0 + r) * idx_stride;
+  // index row of (layer, b, h); KVC_FLAG_SHARED_INDEX: (layer, b)'s row serves every head
+  const int32_t* irow = gidx + (int64_t)((ly->row0 + r) / (shared ? H : 1)) * idx_stride;
   const int64_t obase = ((int64_t)r * n_out + t0) * NC * 16;
   char* ko = static_cast<char*>(ly->k_out) + obase;
   char* vo = static_cast<char*>(ly->v_out) + obase;
@@ -1687,7 +1702,9 @@ __global__ void __launch_bounds__(kGatherThreads)
         src = t;
       } else if (t < sink + nsel) {
         int zi = irow[t - sink];
-        zi = min(max(zi, 0), ly->zone_len - 1);  // never read outside the zone
+        if ((zi < 0 || zi >= ly->zone_len) && status)  // never read outside the zone: clamp
+          atomicOr(status, (uint32_t)KVC_DEV_INDEX_RANGE);
+        zi = min(max(zi, 0), ly->zone_len - 1);
         src = ly->zone_start + zi;
         gat[i] = true;
       } else {
@@ -1805,7 +1822,7 @@ template <int KC, int NT, int NC>
 __global__ void __launch_bounds__(NT, 8)
     select_gather_kernel(const LayerChunk T, int H, int BH, int dt, int order, int algo,
                          const char* __restrict__ norms, int64_t norm_stride, int wave_seg,
-                         int n_cap, int cap) {
+                         int n_cap, int cap, uint32_t* status) {
   typedef typename DTypeTraits<KC>::key_t KeyT;
   constexpr int ESZ = DTypeTraits<KC>::esz;
   constexpr int MAXN = NT == kSelThreads ? kZoneMax : NT * 16;
@@ -1827,13 +1844,180 @@ __global__ void __launch_bounds__(NT, 8)
   }
   uint16_t* sel = reinterpret_cast<uint16_t*>(arrays);  // key region, dead after the chain
   if (selects) {
-    select_body<KC, true, MAXN, NT>(ly, dt, order, algo, nrow, nullptr, sel, arrays, n_cap, cap,
-                                    sc, wave_seg, nullptr);
+    const bool ok = select_body<KC, true, MAXN, NT>(ly, dt, order, algo, nrow, nullptr, sel,
+                                                    arrays, n_cap, cap, sc, wave_seg, nullptr,
+                                                    status);
+    if (!ok) return;  // flagged in *status; the row's output is left unwritten
     __syncthreads();
   }
   with_dt<KC>(dt, [&](auto D) {
     gather_row<D.value, NC, NT, true>(ly, r, H, selects ? sel : nullptr);
   });
+}
+
+// ---------------------------------------------------------------------------------------------
+// h2o_attention heavy hitters: torch's CPU sums restated per output column
+// ---------------------------------------------------------------------------------------------
+// aten cascade_sum (SumKernel.cpp) adds the rows of one output column in one of two orders:
+//   cascade (multi_row_sum): four accumulator levels; rows go one by one into level 0, and after
+//     every 2^p rows (p = max(4, CeilLog2(n) / 4)) level j-1 is folded into level j while the row
+//     counter's j-th p-bit digit is zero; result ((a0 + a1) + a2) + a3.
+//   ilp4 (row_sum): four interleaved lanes (row i -> lane i % 4), each a cascade over n / 4 rows,
+//     leftover rows into lane 0, then ((l0 + l1) + l2) + l3.
+// Which columns take ilp4 depends on the loop calls the reference made (col_class).
+__device__ __forceinline__ int ceil_log2_i(int x) { return x <= 2 ? 1 : 32 - __clz(x - 1); }
+
+template <typename LD>
+__device__ __forceinline__ float cascade_sum(const LD& ld, int n, int off, int mul) {
+  const int lp = max(4, ceil_log2_i(n) / 4);
+  const int step = 1 << lp, mask = step - 1;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int i = 0;
+  while (i + step <= n) {
+    if (step == 16) {  // the common level size: loads first, then the dependent adds
+      float x[16];
+#pragma unroll
+      for (int t = 0; t < 16; ++t) x[t] = ld(off + (i + t) * mul);
+#pragma unroll
+      for (int t = 0; t < 16; ++t) a0 = a0 + x[t];
+      i += 16;
+    } else {
+      for (int t = 0; t < step; ++t, ++i) a0 = a0 + ld(off + i * mul);
+    }
+    a1 = a1 + a0;
+    a0 = 0.f;
+    if ((i & (mask << lp)) == 0) {
+      a2 = a2 + a1;
+      a1 = 0.f;
+      if ((i & (mask << (2 * lp))) == 0) {
+        a3 = a3 + a2;
+        a2 = 0.f;
+      }
+    }
+  }
+  for (; i < n; ++i) a0 = a0 + ld(off + i * mul);
+  a0 = a0 + a1;
+  a0 = a0 + a2;
+  return a0 + a3;
+}
+
+template <typename LD>
+__device__ __forceinline__ float ilp4_sum(const LD& ld, int n) {
+  const int n4 = n >> 2;
+  float p0 = cascade_sum(ld, n4, 0, 4);
+  const float p1 = cascade_sum(ld, n4, 1, 4);
+  const float p2 = cascade_sum(ld, n4, 2, 4);
+  const float p3 = cascade_sum(ld, n4, 3, 4);
+  for (int i = 4 * n4; i < n; ++i) p0 = p0 + ld(i);
+  p0 = p0 + p1;
+  p0 = p0 + p2;
+  return p0 + p3;
+}
+
+// Does column j of `cols` take the ilp4 order?  The reference's loop calls cover the columns in
+// chunks: one call [0, cols) (chunk == 0), or parallel_dim_reduction's thread chunks of `chunk`
+// columns with bounds rounded down to `rnd` columns (128 bytes; the final end stays cols).  In a
+// call of L columns the vectorised loop (L >= vec_min = one Vectorized<scalar_t>) sums whole
+// groups of `group` columns (four Vectorized<float>) with the cascade and the rest with row_sum;
+// a shorter call sums groups of four columns with the cascade and the rest with row_sum.
+__device__ __forceinline__ bool col_ilp(int j, int cols, int chunk, int rnd, int group,
+                                        int vec_min) {
+  int s = 0, e = cols;
+  if (chunk > 0) {
+    const int T = (cols + chunk - 1) / chunk;  // threads that start below cols
+    int t = j / chunk;
+    while (t + 1 < T && ((t + 1) * chunk) / rnd * rnd <= j) ++t;
+    s = (t * chunk) / rnd * rnd;
+    e = t + 1 < T ? ((t + 1) * chunk) / rnd * rnd : cols;
+  }
+  const int L = e - s;
+  const int g = L >= vec_min ? group : 4;
+  return j - s >= L / g * g;
+}
+
+template <int DT>
+__device__ __forceinline__ uint32_t store_bits(float f) {
+  if constexpr (DT == KVC_F32)
+    return f32_to_bits(f);
+  else
+    return bits16_dt<DT>(f);
+}
+template <int DT>
+__device__ __forceinline__ void store_dt(void* base, int64_t i, float f) {
+  if constexpr (DT == KVC_F32)
+    reinterpret_cast<float*>(base)[i] = f;
+  else
+    reinterpret_cast<uint16_t*>(base)[i] = (uint16_t)bits16_dt<DT>(f);
+}
+
+struct AttnChunk {
+  kvc_attn_layer_t l[kArgLayers];
+};
+struct HHChunk {
+  kvc_hh_layer_t l[kArgLayers];
+};
+constexpr int kColThreads = 256;
+
+// update_attention_scores (h2o_attention.py:100-151) for every layer of the chunk: grid
+// (layer * batch * heads rows, column blocks); one thread per key column:
+//   imp = dt(0 + sum_q attn[b,h,q,j])                     attn.sum(dim=2)           (:116)
+//   acc_new = dt(base + imp), base = dt(acc_old*decay) for j < old_len, else 0  (:118-151)
+// Reads of attn are coalesced across the block's columns (q rows of stride attn_stride[2]).
+template <int DT>
+__global__ void __launch_bounds__(kColThreads)
+    attn_accum_kernel(const AttnChunk T, int H, int BH, float decay, int group, int vec_min) {
+  constexpr int ESZ = DTypeTraits<DT>::esz;
+  const kvc_attn_layer_t* ly = T.l + blockIdx.x / BH;
+  const int r = (int)(blockIdx.x % BH);
+  const int j = (int)blockIdx.y * kColThreads + (int)threadIdx.x;
+  const int k = ly->key_len;
+  if (j >= k) return;
+  const int b = r / H, h = r - (r / H) * H;
+  const char* a = static_cast<const char*>(ly->attn) +
+                  ((int64_t)b * ly->attn_stride[0] + (int64_t)h * ly->attn_stride[1] + j) * ESZ;
+  const int64_t qs = ly->attn_stride[2] * ESZ;
+  const auto ld = [&](int i) { return load_dt<DT>(a + (int64_t)i * qs, 0); };
+  const int q = ly->q_len;
+  float s;
+  if (q == 1)
+    s = 0.f + ld(0);  // no reduction: the elementwise out = 0 + x
+  else if (col_ilp(j, k, ly->col_chunk, 128 / ESZ, group, vec_min))
+    s = 0.f + ilp4_sum(ld, q);  // the accumulating store adds to the zero-filled output
+  else
+    s = 0.f + cascade_sum(ld, q, 0, 1);
+  const float imp = round_dt<DT>(s);
+  float base = 0.f;
+  if (j < ly->old_len)
+    base = round_dt<DT>(load_dt<DT>(static_cast<const char*>(ly->acc_old),
+                                    (int)((int64_t)r * ly->old_len + j)) * decay);
+  store_dt<DT>(ly->acc_new, (int64_t)r * k + j, base + imp);
+}
+
+// get_heavy_hitter_indices' head sum (h2o_attention.py:194-198) for every layer of the chunk:
+// grid (layer * batch rows, column blocks); row l*batch + b of `sums` (dtype, row stride
+// `stride`) receives dt(0 + sum_h acc[b, h, m0 + j]) for j < zone_len.
+template <int DT>
+__global__ void __launch_bounds__(kColThreads)
+    head_sum_kernel(const HHChunk T, int H, int B, int group, int vec_min, char* sums,
+                    int64_t stride) {
+  constexpr int ESZ = DTypeTraits<DT>::esz;
+  const int l = (int)(blockIdx.x / B), b = (int)(blockIdx.x % B);
+  const kvc_hh_layer_t* ly = T.l + l;
+  const int j = (int)blockIdx.y * kColThreads + (int)threadIdx.x;
+  const int m = ly->zone_len;
+  if (j >= m) return;
+  const char* a = static_cast<const char*>(ly->acc) +
+                  ((int64_t)b * H * ly->acc_len + ly->zone_start + j) * ESZ;
+  const int64_t hs = (int64_t)ly->acc_len * ESZ;
+  const auto ld = [&](int i) { return load_dt<DT>(a + (int64_t)i * hs, 0); };
+  float s;
+  if (H == 1)
+    s = 0.f + ld(0);
+  else if (col_ilp(j, m, ly->col_chunk, 128 / ESZ, group, vec_min))
+    s = 0.f + ilp4_sum(ld, H);
+  else
+    s = 0.f + cascade_sum(ld, H, 0, 1);
+  store_dt<DT>(sums + (int64_t)blockIdx.x * stride * ESZ, j, s);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1862,6 +2046,9 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
   if (p->batch < 1 || p->heads < 1 || p->head_dim < 1) return KVC_E_ARG;
   if (p->order != KVC_ASC && p->order != KVC_DESC) return KVC_E_ARG;
   if (p->algo != KVC_ALGO_SORT && p->algo != KVC_ALGO_TOPK) return KVC_E_ARG;
+  if ((p->flags & ~(KVC_FLAG_SPLIT_SELECT_GATHER | KVC_FLAG_SHARED_INDEX)) || p->reserved != 0)
+    return KVC_E_ARG;  // unknown flag bits / reserved field: refuse rather than ignore
+  if ((p->flags & KVC_FLAG_SHARED_INDEX) && !p->external_index) return KVC_E_ARG;
   const int es = esize(p->dtype);
   const int rowb = p->head_dim * es;
   if (rowb % 16) return KVC_E_HEADDIM;
@@ -1979,10 +2166,42 @@ static int launch_score(const LayerChunk& T, int nl, int H, int64_t tile_base,
 // `work` = max n_out over the chunk's layers; grid = (rows, token blocks)
 template <int DT, int NC>
 static int launch_gather(const LayerChunk& T, int nl, int H, int BH, const int32_t* idx,
-                         int64_t istride, int64_t work, hipStream_t s) {
+                         int64_t istride, int shared, uint32_t* status, int64_t work,
+                         hipStream_t s) {
   const dim3 grid((unsigned)(nl * BH), (unsigned)((work + kGatherTokens - 1) / kGatherTokens));
   return launch_k(gather_kernel<DT, NC, true>, grid, dim3(kGatherThreads), 0, s, T, H, BH, idx,
-                  istride);
+                  istride, shared, status);
+}
+
+// SELECT over the rows of a chunk (BH rows per layer, workspace row ly->row0 + blockIdx % BH):
+// the LDS kernels (512-thread rows for zones up to kSmallZone, else 1 024-thread rows) or, for
+// zones longer than kZoneMax, the global-scratch kernels (u32 positions beyond kZoneMaxGlobal).
+template <int KC>
+static int launch_select(const LayerChunk& T, int cn, int BH, int dt, int order, int algo,
+                         const char* norms, int64_t nstride, int32_t* idx, int64_t istride,
+                         bool long_zone, char* scratch, uint64_t* stamps, uint32_t* status,
+                         hipStream_t s) {
+  typedef typename DTypeTraits<KC>::key_t KeyT;
+  const dim3 rows_grid((unsigned)(cn * BH));
+  const int n_cap = (int)nstride;  // longest zone of the call, rounded to 64
+  if (long_zone) {
+    const int64_t rb = (int64_t)sel_scratch_row_bytes(n_cap, KC);
+    if (n_cap > kZoneMaxGlobal)  // u32 positions (the call's longest zone decides)
+      return launch_k(select_long_kernel<KC>, rows_grid, dim3(kSelThreads), 0, s, T, BH, dt,
+                      order, algo, norms, nstride, idx, istride, scratch, rb, n_cap, status);
+    return launch_k(select_global_kernel<KC>, rows_grid, dim3(kSelThreads), 0, s, T, BH, dt,
+                    order, algo, norms, nstride, idx, istride, kWaveSeg, scratch, rb, n_cap,
+                    status);
+  }
+  const int ks = (int)sizeof(KeyT);
+  if (n_cap <= kSmallZone) {
+    const int cap = sel_cap(n_cap, ks);
+    return launch_k(select_kernel<KC, kSelThreadsSmall>, rows_grid, dim3(kSelThreadsSmall),
+                    sel_bytes(n_cap, ks, cap), s, T, BH, dt, order, algo, norms, nstride, idx,
+                    istride, kWaveSeg, n_cap, cap, stamps, status);
+  }
+  return launch_k(select_kernel<KC, kSelThreads>, rows_grid, dim3(kSelThreads), 0, s, T, BH, dt,
+                  order, algo, norms, nstride, idx, istride, kWaveSeg, n_cap, 0, stamps, status);
 }
 
 // One chunk of <= kArgLayers layers: SCORE, then SELECT_GATHER (or SELECT and GATHER as two
@@ -2014,48 +2233,153 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
     max_out = layers[l].n_out > max_out ? layers[l].n_out : max_out;
   }
   const bool ext = p->external_index != 0;
+  uint32_t* status = p->device_status;
   int rc = KVC_OK;
   if ((p->phases & KVC_PHASE_SCORE) && tile_end > tile_base && !ext)
     rc = launch_score<DT, NC>(T, cn, H, tile_base, tile_end - tile_base, norms, nstride, s);
   if (rc != KVC_OK) return rc;
-  const dim3 rows_grid((unsigned)(cn * BH));
   const int n_cap = (int)nstride;  // longest zone of the call, rounded to 64
-  if ((p->phases & KVC_PHASE_SELECT) && sel && !ext && long_zone) {
-    char* scratch = w + round_up(info.index_offset + (size_t)info.rows * istride * 4, 256);
-    const int64_t rb = (int64_t)sel_scratch_row_bytes(n_cap, p->dtype);
-    if (n_cap > kZoneMaxGlobal)  // u32 positions (the call's longest zone decides)
-      rc = launch_k(select_long_kernel<KC>, rows_grid, dim3(kSelThreads), 0, s, T, BH, DT,
-                    p->order, p->algo, norms, nstride, idx, istride, scratch, rb, n_cap);
-    else
-      rc = launch_k(select_global_kernel<KC>, rows_grid, dim3(kSelThreads), 0, s, T, BH, DT,
-                    p->order, p->algo, norms, nstride, idx, istride, kWaveSeg, scratch, rb, n_cap);
-  } else if ((p->phases & KVC_PHASE_SELECT) && sel && !ext) {
-    uint64_t* st = stamps ? stamps + (size_t)layers[c0].row0 * 32 : nullptr;
-    const int ks = (int)sizeof(KeyT);
-    const bool small = n_cap <= kSmallZone;
-    const int cap = small ? sel_cap(n_cap, ks) : 0;
-    const size_t lds = small ? sel_bytes(n_cap, ks, cap) : 0;
+  if ((p->phases & KVC_PHASE_SELECT) && sel && !ext) {
     const bool fuse_sg = (p->phases & KVC_PHASE_GATHER) && max_out > 0 && !stamps &&
-                         !(p->flags & KVC_FLAG_SPLIT_SELECT_GATHER);
+                         !long_zone && !(p->flags & KVC_FLAG_SPLIT_SELECT_GATHER);
     if (fuse_sg) {  // this chunk's gather happens inside the select kernel
-      if (small)
+      const dim3 rows_grid((unsigned)(cn * BH));
+      const int ks = (int)sizeof(KeyT);
+      if (n_cap <= kSmallZone) {
+        const int cap = sel_cap(n_cap, ks);
         return launch_k(select_gather_kernel<KC, kSelThreadsSmall, NC>, rows_grid,
-                        dim3(kSelThreadsSmall), lds, s, T, H, BH, DT, p->order, p->algo, norms,
-                        nstride, kWaveSeg, n_cap, cap);
-      return launch_k(select_gather_kernel<KC, kSelThreads, NC>, rows_grid, dim3(kSelThreads),
-                      lds, s, T, H, BH, DT, p->order, p->algo, norms, nstride, kWaveSeg, n_cap, cap);
+                        dim3(kSelThreadsSmall), sel_bytes(n_cap, ks, cap), s, T, H, BH, DT,
+                        p->order, p->algo, norms, nstride, kWaveSeg, n_cap, cap, status);
+      }
+      return launch_k(select_gather_kernel<KC, kSelThreads, NC>, rows_grid, dim3(kSelThreads), 0,
+                      s, T, H, BH, DT, p->order, p->algo, norms, nstride, kWaveSeg, n_cap, 0,
+                      status);
     }
-    if (small)
-      rc = launch_k(select_kernel<KC, kSelThreadsSmall>, rows_grid, dim3(kSelThreadsSmall), lds,
-                    s, T, BH, DT, p->order, p->algo, norms, nstride, idx, istride, kWaveSeg, n_cap,
-                    cap, st);
-    else
-      rc = launch_k(select_kernel<KC, kSelThreads>, rows_grid, dim3(kSelThreads), lds, s, T, BH,
-                    DT, p->order, p->algo, norms, nstride, idx, istride, kWaveSeg, n_cap, cap, st);
+    char* scratch = w + round_up(info.index_offset + (size_t)info.rows * istride * 4, 256);
+    uint64_t* st = stamps ? stamps + (size_t)layers[c0].row0 * 32 : nullptr;
+    rc = launch_select<KC>(T, cn, BH, DT, p->order, p->algo, norms, nstride, idx, istride,
+                           long_zone, scratch, st, status, s);
   }
   if (rc != KVC_OK) return rc;
   if ((p->phases & KVC_PHASE_GATHER) && max_out > 0)
-    rc = launch_gather<DT, NC>(T, cn, H, BH, idx, istride, max_out, s);
+    rc = launch_gather<DT, NC>(T, cn, H, BH, idx, istride,
+                               (p->flags & KVC_FLAG_SHARED_INDEX) ? 1 : 0, status, max_out, s);
+  return rc;
+}
+
+// ---- h2o_attention host side ----------------------------------------------------------------
+static int attn_params_check(const kvc_attn_params_t* p) {
+  if (!p) return KVC_E_ARG;
+  if (p->dtype != KVC_BF16 && p->dtype != KVC_F16 && p->dtype != KVC_F32) return KVC_E_DTYPE;
+  if (p->batch < 1 || p->heads < 1 || p->flags != 0) return KVC_E_ARG;
+  if (p->vec_bytes < 16 || p->vec_bytes > 64 || p->vec_bytes % 16) return KVC_E_ARG;
+  if ((int64_t)p->batch * p->heads > 0x7FFFFFFF / kArgLayers) return KVC_E_ARG;
+  return KVC_OK;
+}
+
+static int accumulate_impl(const kvc_attn_params_t* p, const kvc_attn_layer_t* layers, int nl,
+                           hipStream_t s) {
+  int rc = attn_params_check(p);
+  if (rc != KVC_OK) return rc;
+  if (nl < 0 || (nl > 0 && !layers)) return KVC_E_ARG;
+  const int es = esize(p->dtype);
+  for (int l = 0; l < nl; ++l) {
+    const kvc_attn_layer_t& y = layers[l];
+    if (!y.attn || !y.acc_new || y.q_len < 1 || y.key_len < 1 || y.old_len < 0 ||
+        y.old_len > y.key_len || (y.old_len > 0 && !y.acc_old) || y.col_chunk < 0 ||
+        ((uintptr_t)y.attn | (uintptr_t)y.acc_new | (uintptr_t)y.acc_old) % es)
+      return KVC_E_ARG;
+    if ((y.key_len + kColThreads - 1) / kColThreads > 65535) return KVC_E_TOO_LONG;
+  }
+  const int H = p->heads, BH = p->batch * p->heads;
+  const int group = 4 * (p->vec_bytes / 4), vec_min = p->vec_bytes / es;
+  for (int c0 = 0; c0 < nl && rc == KVC_OK; c0 += kArgLayers) {
+    const int cn = nl - c0 < kArgLayers ? nl - c0 : kArgLayers;
+    AttnChunk T;
+    memcpy(T.l, layers + c0, (size_t)cn * sizeof(kvc_attn_layer_t));
+    int kmax = 0;
+    for (int l = 0; l < cn; ++l) kmax = T.l[l].key_len > kmax ? T.l[l].key_len : kmax;
+    const dim3 grid((unsigned)(cn * BH), (unsigned)((kmax + kColThreads - 1) / kColThreads));
+    rc = with_dtype(p->dtype, [&](auto dt) {
+      return launch_k(attn_accum_kernel<decltype(dt)::value>, grid, dim3(kColThreads), 0, s, T,
+                      H, BH, p->decay, group, vec_min);
+    });
+  }
+  return rc;
+}
+
+// Workspace of kvc_heavy_hitters: head-summed rows [layers * batch, nstride] of dtype, then the
+// global selection scratch rows when a zone is longer than kZoneMax.
+static int hh_layout(const kvc_attn_params_t* p, const kvc_hh_layer_t* layers, int nl,
+                     int64_t* nstride, size_t* sums_bytes, size_t* total) {
+  int rc = attn_params_check(p);
+  if (rc != KVC_OK) return rc;
+  if (nl < 0 || (nl > 0 && !layers)) return KVC_E_ARG;
+  int64_t mmax = 1;
+  for (int l = 0; l < nl; ++l) {
+    const kvc_hh_layer_t& y = layers[l];
+    if (!y.acc || y.acc_len < 1 || y.zone_start < 0 || y.zone_len < 1 ||
+        (int64_t)y.zone_start + y.zone_len > y.acc_len || y.n_select < 0 ||
+        y.n_select > y.zone_len || y.col_chunk < 0 || y.reserved != 0 ||
+        (uintptr_t)y.acc % esize(p->dtype))
+      return KVC_E_ARG;
+    if (y.zone_len > kZoneMaxLong) return KVC_E_TOO_LONG;
+    mmax = y.zone_len > mmax ? y.zone_len : mmax;
+  }
+  const int64_t rows = (int64_t)nl * p->batch;
+  *nstride = (int64_t)round_up((size_t)mmax, kTile);
+  *sums_bytes = round_up((size_t)rows * *nstride * esize(p->dtype), 256);
+  *total = *sums_bytes;
+  if (mmax > kZoneMax) *total += (size_t)rows * sel_scratch_row_bytes((int)*nstride, p->dtype);
+  return KVC_OK;
+}
+
+static int heavy_hitters_impl(const kvc_attn_params_t* p, const kvc_hh_layer_t* layers, int nl,
+                              int32_t* out, int64_t ostride, char* w, size_t wbytes,
+                              hipStream_t s) {
+  int64_t nstride;
+  size_t sums_bytes, total;
+  int rc = hh_layout(p, layers, nl, &nstride, &sums_bytes, &total);
+  if (rc != KVC_OK) return rc;
+  if (nl == 0) return KVC_OK;
+  if (!w || wbytes < total) return KVC_E_WORKSPACE;
+  if (!out) return KVC_E_ARG;
+  for (int l = 0; l < nl; ++l)
+    if (layers[l].n_select > ostride) return KVC_E_ARG;
+  const int B = p->batch, H = p->heads, es = esize(p->dtype);
+  const int group = 4 * (p->vec_bytes / 4), vec_min = p->vec_bytes / es;
+  for (int c0 = 0; c0 < nl && rc == KVC_OK; c0 += kArgLayers) {
+    const int cn = nl - c0 < kArgLayers ? nl - c0 : kArgLayers;
+    HHChunk T;
+    memcpy(T.l, layers + c0, (size_t)cn * sizeof(kvc_hh_layer_t));
+    LayerChunk S;  // the selection rows: zone = the head-summed row, chunk-local row0
+    memset(&S, 0, sizeof(S));
+    int mmax = 0;
+    bool long_zone = false;
+    for (int l = 0; l < cn; ++l) {
+      S.l[l].zone_len = T.l[l].zone_len;
+      S.l[l].n_select = T.l[l].n_select;
+      S.l[l].seq_len = T.l[l].zone_len;
+      S.l[l].score_mode = KVC_SCORE_NORM;
+      S.l[l].row0 = l * B;
+      mmax = T.l[l].zone_len > mmax ? T.l[l].zone_len : mmax;
+      long_zone |= T.l[l].zone_len > kZoneMax;
+    }
+    char* sums = w + (size_t)c0 * B * nstride * es;
+    char* scratch = w + sums_bytes + (size_t)c0 * B * sel_scratch_row_bytes((int)nstride, p->dtype);
+    int32_t* o = out + (int64_t)c0 * B * ostride;
+    const dim3 grid((unsigned)(cn * B), (unsigned)((mmax + kColThreads - 1) / kColThreads));
+    rc = with_dtype(p->dtype, [&](auto dt) {
+      constexpr int DT = decltype(dt)::value;
+      constexpr int KC = DT == KVC_F32 ? KVC_F32 : KVC_BF16;
+      int r = launch_k(head_sum_kernel<DT>, grid, dim3(kColThreads), 0, s, T, H, B, group,
+                       vec_min, sums, nstride);
+      if (r != KVC_OK) return r;
+      // torch.topk(largest=True) + torch.sort: the descending TOPK selection, ascending indices
+      return launch_select<KC>(S, cn, B, DT, KVC_DESC, KVC_ALGO_TOPK, sums, nstride, o, ostride,
+                               long_zone, scratch, nullptr, p->device_status, s);
+    });
+  }
   return rc;
 }
 
@@ -2115,6 +2439,29 @@ int kvc_compress(const kvc_params_t* params, kvc_layer_t* layers, int num_layers
   const int rc = kvc::plan_impl(params, layers, num_layers, &info, true);
   if (rc != KVC_OK) return rc;
   return kvc_launch(params, layers, num_layers, ws, ws_bytes, stream);
+}
+
+int kvc_attn_accumulate(const kvc_attn_params_t* params, const kvc_attn_layer_t* layers,
+                        int num_layers, kvc_stream_t stream) {
+  return kvc::accumulate_impl(params, layers, num_layers, reinterpret_cast<hipStream_t>(stream));
+}
+
+int kvc_hh_workspace(const kvc_attn_params_t* params, const kvc_hh_layer_t* layers,
+                     int num_layers, size_t* bytes) {
+  int64_t nstride;
+  size_t sums, total;
+  if (!bytes) return KVC_E_ARG;
+  const int rc = kvc::hh_layout(params, layers, num_layers, &nstride, &sums, &total);
+  if (rc == KVC_OK) *bytes = total;
+  return rc;
+}
+
+int kvc_heavy_hitters(const kvc_attn_params_t* params, const kvc_hh_layer_t* layers,
+                      int num_layers, int32_t* out_idx, int64_t out_row_stride, void* workspace,
+                      size_t workspace_bytes, kvc_stream_t stream) {
+  return kvc::heavy_hitters_impl(params, layers, num_layers, out_idx, out_row_stride,
+                                 static_cast<char*>(workspace), workspace_bytes,
+                                 reinterpret_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

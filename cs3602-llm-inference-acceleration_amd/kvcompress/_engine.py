@@ -275,11 +275,38 @@ class _PlanCache:
 plan_cache = _PlanCache()
 
 
-def _params(dtype, B, H, D, order, algo, external):
+_status_words = {}
+
+
+def status_word(device):
+    """The per-device word the kernels OR enum kvc_device_status bits into (zeroed once; sticky).
+    Read it with device_status()."""
+    w = _status_words.get(device)
+    if w is None:
+        w = torch.zeros(1, dtype=torch.int32, device=torch.device("cuda", device))
+        _status_words[device] = w
+    return w
+
+
+def device_status(device=None, clear=False):
+    """Synchronises `device` and returns the kvc_device_status bits its kernels have reported
+    since the last clear (0 = none).  KVC_DEV_SELECT_BOUNDS means a selection row's output is
+    unspecified; KVC_DEV_INDEX_RANGE that a caller-provided index was clamped into its zone."""
+    device = torch.cuda.current_device() if device is None else device
+    w = status_word(device)
+    v = int(w.item())
+    if clear:
+        w.zero_()
+    return v
+
+
+def _params(dtype, B, H, D, order, algo, external, shared=False):
+    flags = (N.FLAG_SPLIT_SELECT_GATHER if split_select_gather else 0) | \
+        (N.FLAG_SHARED_INDEX if shared else 0)
     return N.Params(dtype=_SUPPORTED[dtype], batch=B, heads=H, head_dim=D, order=order,
                     algo=algo, phases=N.PHASE_GATHER if external else N.PHASE_ALL,
-                    external_index=1 if external else 0,
-                    flags=N.FLAG_SPLIT_SELECT_GATHER if split_select_gather else 0)
+                    external_index=1 if external else 0, flags=flags,
+                    device_status=status_word(torch.cuda.current_device()).data_ptr())
 
 
 def _outputs(device, dtype, B, H, D, n_outs):
@@ -367,7 +394,9 @@ def _plan_plain(dtype, B, H, D, order, algo, segs):
     return table, info, ws, p, n_outs
 
 
-def _run_general(device, dtype, B, H, D, js, out_list, order, algo, external, stream):
+def _build_table(device, dtype, B, H, D, js):
+    """Layer table of a group (pointers, strides, segment bounds) and its output tensors; `keep`
+    holds prepared (contiguous) input copies alive until the launch has been issued."""
     es = _ESIZE[dtype]
     rows_ok = (D * es) % 16 == 0
     n_outs = [j.sink_len + j.n_select + j.tail_len for j in js]
@@ -390,7 +419,36 @@ def _run_general(device, dtype, B, H, D, js, out_list, order, algo, external, st
         rows.append((kp, vp, int(kops[i]), int(vops[i]), kst[:3], vst[:3], k.shape[2],
                      j.zone_start, j.zone_len, j.n_select, j.sink_len, j.tail_start, j.tail_len,
                      j.pool_kernel, j.score_mode, 0, 0, 0, 0))
-    table = np.array(rows, dtype=N.LAYER_DTYPE)
+    return np.array(rows, dtype=N.LAYER_DTYPE), kos, vos, keep
+
+
+def execute_shared(jobs: List[Segments], out_list: list, fill):
+    """External-index GATHER whose index row (layer, b) serves every head of the layer
+    (KVC_FLAG_SHARED_INDEX: h2o_attention's heavy hitters, one index list per layer).  Per group,
+    `fill(js, index_region_ptr, row_stride, stream)` writes row (i * B + b) of job i before the
+    copy kernel is enqueued on the same stream."""
+    groups = {}
+    for j in jobs:
+        B, H, _, D = _check_tensors(j)
+        groups.setdefault((j.keys.get_device(), j.keys.dtype, B, H, D), []).append(j)
+    for (device, dtype, B, H, D), js in groups.items():
+        with torch.cuda.device(device):
+            stream = torch.cuda.current_stream(device)
+            table, kos, vos, keep = _build_table(device, dtype, B, H, D, js)
+            p = _params(dtype, B, H, D, N.KVC_ASC, N.KVC_ALGO_SORT, True, shared=True)
+            rc, info = N.plan(p, table)
+            N.check(rc, "kvc_plan")
+            ws = torch.empty(max(int(info.workspace_bytes), 256), dtype=torch.uint8,
+                             device=torch.device("cuda", device))
+            fill(js, ws.data_ptr() + int(info.index_offset), int(info.index_row_stride), stream)
+            _launch(p, table, ws, info, stream, p.phases)
+            del keep
+        for j, ko, vo in zip(js, kos, vos):
+            out_list[j.layer_idx] = (ko, vo)
+
+
+def _run_general(device, dtype, B, H, D, js, out_list, order, algo, external, stream):
+    table, kos, vos, keep = _build_table(device, dtype, B, H, D, js)
     # One launch (score, select, gather kernels) for every layer of the group.  (Pipelining
     # layer chunks over two streams -- score of chunk c+1 beside select of chunk c -- was
     # measured slower at 2/4/8 chunks: profiles/r01_pipeline_sweep.json.)

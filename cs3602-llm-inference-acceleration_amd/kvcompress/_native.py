@@ -18,8 +18,9 @@ KVC_ASC, KVC_DESC = 0, 1
 KVC_ALGO_SORT, KVC_ALGO_TOPK = 0, 1
 KVC_SCORE_NORM, KVC_SCORE_SNAPKV = 0, 1
 PHASE_SCORE, PHASE_SELECT, PHASE_GATHER, PHASE_ALL = 1, 2, 4, 7
-FLAG_SPLIT_SELECT_GATHER = 1
-ABI_VERSION = 2
+FLAG_SPLIT_SELECT_GATHER, FLAG_SHARED_INDEX = 1, 2
+DEV_SELECT_BOUNDS, DEV_INDEX_RANGE = 1, 2  # enum kvc_device_status bits
+ABI_VERSION = 3
 KVC_E_TOO_LONG = -5
 
 # struct kvc_layer (include/kvc.h) -- 136 bytes, checked against kvc_layer_struct_size()
@@ -33,12 +34,31 @@ LAYER_DTYPE = np.dtype([
 ])
 assert LAYER_DTYPE.itemsize == 136
 
+# struct kvc_attn_layer / kvc_hh_layer (include/kvc.h: h2o_attention heavy hitters)
+ATTN_LAYER_DTYPE = np.dtype([
+    ("attn", "<u8"), ("attn_stride", "<i8", (3,)), ("acc_old", "<u8"), ("acc_new", "<u8"),
+    ("q_len", "<i4"), ("key_len", "<i4"), ("old_len", "<i4"), ("col_chunk", "<i4"),
+])
+assert ATTN_LAYER_DTYPE.itemsize == 64
+HH_LAYER_DTYPE = np.dtype([
+    ("acc", "<u8"), ("acc_len", "<i4"), ("zone_start", "<i4"), ("zone_len", "<i4"),
+    ("n_select", "<i4"), ("col_chunk", "<i4"), ("reserved", "<i4"),
+])
+assert HH_LAYER_DTYPE.itemsize == 32
+
 
 class Params(ctypes.Structure):
     _fields_ = [("dtype", ctypes.c_int32), ("batch", ctypes.c_int32), ("heads", ctypes.c_int32),
                 ("head_dim", ctypes.c_int32), ("order", ctypes.c_int32), ("algo", ctypes.c_int32),
                 ("phases", ctypes.c_int32), ("external_index", ctypes.c_int32),
-                ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("device_status", ctypes.c_void_p)]
+
+
+class AttnParams(ctypes.Structure):
+    _fields_ = [("dtype", ctypes.c_int32), ("batch", ctypes.c_int32), ("heads", ctypes.c_int32),
+                ("vec_bytes", ctypes.c_int32), ("decay", ctypes.c_float),
+                ("flags", ctypes.c_int32), ("device_status", ctypes.c_void_p)]
 
 
 class PlanInfo(ctypes.Structure):
@@ -50,7 +70,8 @@ class PlanInfo(ctypes.Structure):
 
 
 EXPORTS = ("kvc_version", "kvc_layer_struct_size", "kvc_max_zone_len", "kvc_status_string",
-           "kvc_plan", "kvc_launch", "kvc_compress")
+           "kvc_plan", "kvc_launch", "kvc_compress", "kvc_attn_accumulate", "kvc_hh_workspace",
+           "kvc_heavy_hitters")
 
 _lib = None
 
@@ -81,6 +102,14 @@ def lib():
     L.kvc_launch.argtypes = [ctypes.POINTER(Params), vp, i32, vp, ctypes.c_size_t, vp]
     L.kvc_compress.restype = i32
     L.kvc_compress.argtypes = [ctypes.POINTER(Params), vp, i32, vp, ctypes.c_size_t, vp]
+    L.kvc_attn_accumulate.restype = i32
+    L.kvc_attn_accumulate.argtypes = [ctypes.POINTER(AttnParams), vp, i32, vp]
+    L.kvc_hh_workspace.restype = i32
+    L.kvc_hh_workspace.argtypes = [ctypes.POINTER(AttnParams), vp, i32,
+                                   ctypes.POINTER(ctypes.c_size_t)]
+    L.kvc_heavy_hitters.restype = i32
+    L.kvc_heavy_hitters.argtypes = [ctypes.POINTER(AttnParams), vp, i32, vp, ctypes.c_int64, vp,
+                                    ctypes.c_size_t, vp]
     if L.kvc_version() != ABI_VERSION or L.kvc_layer_struct_size() != LAYER_DTYPE.itemsize:
         raise NativeLibraryError("libkvc.so ABI mismatch; rebuild it")
     _lib = L
@@ -105,3 +134,20 @@ def plan(params, table):
 def launch(params, table, ws_ptr, ws_bytes, stream_ptr):
     return lib().kvc_launch(ctypes.byref(params), table.ctypes.data, len(table), ws_ptr, ws_bytes,
                             stream_ptr)
+
+
+def attn_accumulate(params, table, stream_ptr):
+    return lib().kvc_attn_accumulate(ctypes.byref(params), table.ctypes.data, len(table),
+                                     stream_ptr)
+
+
+def hh_workspace(params, table):
+    n = ctypes.c_size_t()
+    rc = lib().kvc_hh_workspace(ctypes.byref(params), table.ctypes.data, len(table),
+                                ctypes.byref(n))
+    return rc, n.value
+
+
+def heavy_hitters(params, table, out_ptr, out_stride, ws_ptr, ws_bytes, stream_ptr):
+    return lib().kvc_heavy_hitters(ctypes.byref(params), table.ctypes.data, len(table), out_ptr,
+                                   out_stride, ws_ptr, ws_bytes, stream_ptr)

@@ -1,26 +1,54 @@
 """H2O with attention-score heavy hitters (reference: kvcompress/methods/h2o_attention.py).
 
-The manager keeps the reference's per-layer accumulated attention (sum over queries, exponential
-decay, zero-extension, reset when the cache shrank) and picks heavy hitters as the top-k of the
-head-summed middle region (h2o_attention.py:84-213).  That bookkeeping is a few small torch ops
-on the attention tensors' own device -- the same ops as the reference, so the same results on the
-same device.  The compaction -- sinks ++ K/V rows of the heavy hitters (one index list shared by
-every head) ++ recent window, for every layer of the call -- runs as one HIP engine launch
-(external-index GATHER).  Without a manager the reference falls back to L2-norm heavy hitters,
-which is exactly h2o_l2's selection: the engine's score / select / gather path.
+The manager keeps the reference's per-layer accumulated attention (h2o_attention.py:84-213) and
+every piece of its arithmetic runs on the HIP engine with the CPU reference's exact results:
+
+  update_attention_scores   kvc_attn_accumulate: acc = dt((acc*decay | 0) + dt(attn.sum(dim=2)))
+                            for all layers of the call in one kernel, each column's q-sum in
+                            torch CPU's addition order (cascade_sum; _cpu_order.py)
+  get_heavy_hitter_indices  kvc_heavy_hitters: the head sum acc[:, :, m0:m1].sum(dim=1) in the
+                            same order, then the reference-exact top-k set (std::nth_element /
+                            std::partial_sort tie order, KVC_ALGO_TOPK) as ascending indices
+  h2o_attention_compress    heavy hitters of every layer written straight into the index region
+                            of one gather launch (KVC_FLAG_SHARED_INDEX: one list per layer,
+                            shared by all heads), which copies sinks ++ heavy ++ recent of K/V
+
+Without a manager the reference falls back to L2-norm heavy hitters, which is exactly h2o_l2's
+selection: the engine's score / select / gather path.  Tensors must be on a ROCm device (bf16,
+fp16 or fp32); there is no CPU path.
 """
 from typing import Dict, List, Optional, Tuple
 
+import numpy as np
 import torch
 
+from .. import _cpu_order as CO
 from .. import _engine as E
 from .. import _native as N
 from ..utils import normalize_kv_cache
 
+_DT = {torch.bfloat16: N.KVC_BF16, torch.float16: N.KVC_F16, torch.float32: N.KVC_F32}
+
+
+def _attn_params(dtype, B, H, decay, device):
+    return N.AttnParams(dtype=_DT[dtype], batch=B, heads=H, vec_bytes=CO.SUM_VEC_BYTES,
+                        decay=float(np.float32(decay)), flags=0,
+                        device_status=E.status_word(device).data_ptr())
+
+
+def _check_gpu(t, what):
+    if not t.is_cuda:
+        raise RuntimeError(f"kvcompress (MI355X HIP engine): {what} is on {t.device}; the "
+                           "h2o_attention scoring runs on ROCm GPU tensors only (no CPU fallback).")
+    if t.dtype not in _DT:
+        raise TypeError(f"kvcompress (MI355X HIP engine): {what} must be bfloat16, float16 or "
+                        f"float32, got {t.dtype}")
+
 
 class H2OAttentionManager:
-    """Accumulated attention per layer (h2o_attention.py:27-213): same constructor, state and
-    methods as the reference."""
+    """Accumulated attention per layer (h2o_attention.py:28-213): same constructor, state and
+    methods as the reference.  `reduction_threads` (extension, default None = the process's
+    torch.get_num_threads()) is the thread count whose CPU reduction order the sums reproduce."""
 
     def __init__(self, start_size: int = 4, heavy_hitter_size: int = 64, recent_size: int = 444,
                  num_layers: int = 32, num_heads: int = 32, decay_factor: float = 0.9,
@@ -36,55 +64,120 @@ class H2OAttentionManager:
         self.accumulated_attention: Dict[int, torch.Tensor] = {}
         self.token_positions: Dict[int, torch.Tensor] = {}
         self.current_seq_len = 0
+        self.reduction_threads: Optional[int] = None
 
     def reset(self):
         self.accumulated_attention = {}
         self.token_positions = {}
         self.current_seq_len = 0
 
+    def _threads(self):
+        return self.reduction_threads or CO.threads()
+
     def update_attention_scores(self, attentions, skip_layers: List[int] = []):
-        """h2o_attention.py:84-153: acc <- acc*decay (zero-extended to the new key length, or
-        reset if the cache shrank) + attention summed over queries."""
+        """h2o_attention.py:84-153 for every given layer in one engine launch per
+        (device, dtype, B, H) group: acc <- acc*decay (zero-extended to the new key length; reset
+        to zeros if the cache shrank) + attention summed over queries."""
         if attentions is None:
             return
+        groups = {}
+        threads = self._threads()
         for layer_idx, attn in enumerate(attentions):
             if layer_idx in skip_layers or attn is None:
                 continue
-            b, h, _, key_len = attn.shape
-            importance = attn.sum(dim=2)
+            b, h, q, key_len = attn.shape
+            _check_gpu(attn, f"attention of layer {layer_idx}")
+            if attn.stride(3) != 1 or attn.data_ptr() % attn.element_size():
+                attn = attn.contiguous()
             acc = self.accumulated_attention.get(layer_idx)
-            if acc is None:
-                acc = torch.zeros(b, h, key_len, device=attn.device, dtype=attn.dtype)
-            elif acc.size(-1) < key_len:
-                pad = torch.zeros(b, h, key_len - acc.size(-1), device=attn.device,
-                                  dtype=attn.dtype)
-                acc = torch.cat([acc * self.decay_factor, pad], dim=-1)
-            elif acc.size(-1) > key_len:
-                acc = torch.zeros(b, h, key_len, device=attn.device, dtype=attn.dtype)
-            else:
-                acc = acc * self.decay_factor
-            self.accumulated_attention[layer_idx] = acc + importance
+            old = None
+            if acc is not None and acc.size(-1) <= key_len:  # decay (and zero-extend) (:124-146)
+                if acc.dtype != attn.dtype or acc.device != attn.device or \
+                        acc.shape[:2] != attn.shape[:2]:
+                    raise NotImplementedError(
+                        f"layer {layer_idx}: accumulated attention {acc.dtype}/{acc.device}/"
+                        f"{tuple(acc.shape)} does not match the new attention "
+                        f"{attn.dtype}/{attn.device}/{tuple(attn.shape)}")
+                old = acc.contiguous()
+            # acc.size(-1) > key_len: reset to zeros (:138-144) -- old stays None
+            key = (attn.get_device(), attn.dtype, b, h)
+            groups.setdefault(key, []).append(
+                (layer_idx, attn, old, CO.attn_sum_chunk(attn, threads)))
             self.current_seq_len = key_len
+        for (device, dtype, b, h), jobs in groups.items():
+            with torch.cuda.device(device):
+                sizes = [b * h * a.size(3) for _, a, _, _ in jobs]
+                buf = torch.empty(sum(sizes), dtype=dtype, device=torch.device("cuda", device))
+                accs = [t.view(b, h, a.size(3)) for t, (_, a, _, _) in zip(buf.split(sizes), jobs)]
+                table = np.zeros(len(jobs), dtype=N.ATTN_LAYER_DTYPE)
+                for i, ((li, a, old, chunk), acc) in enumerate(zip(jobs, accs)):
+                    table[i] = (a.data_ptr(), a.stride()[:3],
+                                old.data_ptr() if old is not None else 0, acc.data_ptr(),
+                                a.size(2), a.size(3), old.size(-1) if old is not None else 0,
+                                chunk)
+                p = _attn_params(dtype, b, h, self.decay_factor, device)
+                rc = N.attn_accumulate(p, table, torch.cuda.current_stream(device).cuda_stream)
+                N.check(rc, "kvc_attn_accumulate")
+                for (li, _, _, _), acc in zip(jobs, accs):
+                    self.accumulated_attention[li] = acc
+
+    def _hh_row(self, layer_idx, seq_len):
+        """(acc, m0, m, k) of a layer's heavy-hitter selection (h2o_attention.py:183-206), or
+        None when the middle region is empty."""
+        acc = self.accumulated_attention[layer_idx]
+        attn_len = acc.shape[-1]
+        m0, m1 = self.start_size, min(seq_len, attn_len) - self.recent_size
+        if m1 <= m0:
+            return None
+        return acc, m0, m1 - m0, min(self.heavy_hitter_size, m1 - m0)
 
     def get_heavy_hitter_indices(self, layer_idx: int, seq_len: int) -> torch.Tensor:
-        """h2o_attention.py:155-213: ascending middle-local indices of the heavy hitters."""
-        acc = self.accumulated_attention.get(layer_idx)
-        if acc is None:  # no attention yet: evenly spaced middle positions
+        """h2o_attention.py:156-213: ascending middle-local indices of the heavy hitters ([k], or
+        [B, k] for batch > 1), computed by the engine."""
+        if layer_idx not in self.accumulated_attention:  # evenly spaced middle positions
             m0, m1 = self.start_size, seq_len - self.recent_size
             if m1 <= m0:
                 return torch.tensor([], dtype=torch.long)
             step = max(1, (m1 - m0) // self.heavy_hitter_size)
             return torch.arange(0, m1 - m0, step)[:self.heavy_hitter_size]
-        b, _, attn_len = acc.shape
-        m0, m1 = self.start_size, min(seq_len, attn_len) - self.recent_size
-        if m1 <= m0:
+        acc = self.accumulated_attention[layer_idx]
+        row = self._hh_row(layer_idx, seq_len)
+        if row is None:
             return torch.tensor([], dtype=torch.long, device=acc.device)
-        agg = acc[:, :, m0:m1].sum(dim=1)
-        if b == 1:
-            agg = agg.squeeze(0)
-        _, top = torch.topk(agg, min(self.heavy_hitter_size, m1 - m0), dim=-1)
-        top, _ = torch.sort(top, dim=-1)
-        return top
+        B = acc.shape[0]
+        k = row[3]
+        out = torch.empty((B, max(k, 1)), dtype=torch.int32, device=acc.device)
+        run_heavy_hitters(self, [row], out.data_ptr(), out.size(1),
+                          torch.cuda.current_stream(acc.device))
+        top = out[:, :k].long()
+        return top.squeeze(0) if B == 1 else top
+
+
+def run_heavy_hitters(mgr, rows, out_ptr, out_stride, stream):
+    """kvc_heavy_hitters over `rows` [(acc, m0, m, k)] (one dtype / batch / heads / device):
+    row i * B + b of the int32 array at out_ptr (row stride out_stride) receives the k ascending
+    indices."""
+    acc0 = rows[0][0]
+    _check_gpu(acc0, "accumulated attention")
+    B, H = acc0.shape[:2]
+    threads = mgr._threads()
+    table = np.zeros(len(rows), dtype=N.HH_LAYER_DTYPE)
+    keep = []
+    for i, (acc, m0, m, k) in enumerate(rows):
+        if acc.dtype != acc0.dtype or acc.shape[:2] != (B, H) or acc.device != acc0.device:
+            raise NotImplementedError("heavy hitters of layers with different dtype / batch / "
+                                      "heads / device in one call")
+        acc = acc.contiguous()
+        keep.append(acc)
+        table[i] = (acc.data_ptr(), acc.shape[-1], m0, m, k,
+                    CO.head_sum_chunk(B, H, m, acc.element_size(), threads), 0)
+    device = acc0.get_device()
+    p = _attn_params(acc0.dtype, B, H, mgr.decay_factor, device)
+    rc, nbytes = N.hh_workspace(p, table)
+    N.check(rc, "kvc_hh_workspace")
+    ws = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=acc0.device)
+    rc = N.heavy_hitters(p, table, out_ptr, out_stride, ws.data_ptr(), nbytes, stream.cuda_stream)
+    N.check(rc, "kvc_heavy_hitters")
 
 
 def h2o_attention_compress(past_key_values, attention_scores: Optional[Tuple] = None,
@@ -92,14 +185,14 @@ def h2o_attention_compress(past_key_values, attention_scores: Optional[Tuple] = 
                            start_size: int = 4, heavy_hitter_size: int = 64,
                            recent_size: int = 444, skip_layers: List[int] = [],
                            **kwargs) -> List[Tuple[torch.Tensor, torch.Tensor]]:
-    """h2o_attention.py:216-376."""
+    """h2o_attention.py:216-363."""
     past_key_values = list(normalize_kv_cache(past_key_values))
     if not past_key_values:
         return past_key_values
     total_cache_size = start_size + heavy_hitter_size + recent_size
     if h2o_manager is not None and attention_scores is not None:
         h2o_manager.update_attention_scores(attention_scores, skip_layers)
-    ext_jobs, norm_jobs = [], []
+    hh_jobs, host_jobs, norm_jobs = [], [], []  # (Segments, hh row | host indices)
     for layer_idx, (keys, values) in enumerate(past_key_values):
         seq_len = keys.size(2)
         if seq_len <= total_cache_size or layer_idx in skip_layers:
@@ -108,33 +201,91 @@ def h2o_attention_compress(past_key_values, attention_scores: Optional[Tuple] = 
         sink = E.py_slice(seq_len, None, start_size)[1]
         t0, tl = E.py_slice(seq_len, -recent_size)
         middle_start, middle_end = start_size, seq_len - recent_size
-        jobs = ext_jobs if h2o_manager is not None else norm_jobs
         if middle_end <= middle_start:  # sinks ++ recent (StreamingLLM fallback)
-            jobs.append(E.Segments(layer_idx, keys, values, sink_len=sink, tail_start=t0,
-                                   tail_len=tl))
+            seg = E.Segments(layer_idx, keys, values, sink_len=sink, tail_start=t0, tail_len=tl)
+            (host_jobs if h2o_manager is not None else norm_jobs).append((seg, None))
             continue
         z0, zl = E.py_slice(seq_len, middle_start, middle_end)
         if h2o_manager is None:  # L2-norm heavy hitters (= h2o_l2's selection)
-            norm_jobs.append(E.Segments(layer_idx, keys, values, sink_len=sink, zone_start=z0,
-                                        zone_len=zl,
-                                        n_select=len(range(zl)[:min(heavy_hitter_size, zl)]),
-                                        tail_start=t0, tail_len=tl))
+            norm_jobs.append((E.Segments(layer_idx, keys, values, sink_len=sink, zone_start=z0,
+                                         zone_len=zl,
+                                         n_select=len(range(zl)[:min(heavy_hitter_size, zl)]),
+                                         tail_start=t0, tail_len=tl), None))
             continue
-        idx = h2o_manager.get_heavy_hitter_indices(layer_idx, seq_len)
+        seg = E.Segments(layer_idx, keys, values, sink_len=sink, zone_start=z0, zone_len=zl,
+                         tail_start=t0, tail_len=tl)
+        if layer_idx in h2o_manager.accumulated_attention:
+            acc = h2o_manager.accumulated_attention[layer_idx]
+            row = h2o_manager._hh_row(layer_idx, seq_len)
+            if row is not None and acc.shape[0] == 1:
+                # heavy_indices[:num] (:318-321): the first num of the k ascending indices; the
+                # clamp to the middle (:324) never binds when the manager's middle fits in it
+                seg.n_select = min(row[3], heavy_hitter_size, zl)
+                hh_jobs.append((seg, row))
+                continue
+            idx = h2o_manager.get_heavy_hitter_indices(layer_idx, seq_len)
+        else:
+            idx = h2o_manager.get_heavy_hitter_indices(layer_idx, seq_len)
         num = min(len(idx), heavy_hitter_size, zl)
-        ext = None
         if num > 0 and len(idx) > 0:
             idx = idx[:num].clamp(0, zl - 1).to(keys.device)
             # the reference's index expansion (same shape rules / errors), shared by all heads
-            ext = idx.unsqueeze(0).unsqueeze(0).unsqueeze(-1).expand(b, h, num, d)[..., 0]
+            idx.unsqueeze(0).unsqueeze(0).unsqueeze(-1).expand(b, h, num, d)
+            seg.n_select = num
+            host_jobs.append((seg, idx))
         else:
-            num = 0
-        ext_jobs.append(E.Segments(layer_idx, keys, values, sink_len=sink, zone_start=z0,
-                                   zone_len=zl, n_select=num, tail_start=t0, tail_len=tl,
-                                   ext_index=ext))
-    E.execute(ext_jobs, past_key_values, N.KVC_ASC, N.KVC_ALGO_SORT)
-    E.execute(norm_jobs, past_key_values, N.KVC_ASC, N.KVC_ALGO_SORT)
+            host_jobs.append((seg, None))
+    if hh_jobs or host_jobs:
+        _compact_shared(h2o_manager, hh_jobs + host_jobs, len(hh_jobs), past_key_values)
+    E.execute([s for s, _ in norm_jobs], past_key_values, N.KVC_ASC, N.KVC_ALGO_SORT)
     return past_key_values
+
+
+def _compact_shared(mgr, jobs, n_hh, out_list):
+    """One shared-index gather for the manager path: the index rows of the first n_hh jobs come
+    from kvc_heavy_hitters (written in place when every row fits), the rest from host indices.
+    Within each engine group the heavy-hitter jobs keep their leading positions."""
+    idx_of = {s.layer_idx: extra for s, extra in jobs}
+    hh_layers = {s.layer_idx for s, _ in jobs[:n_hh]}
+
+    def fill(js, region, stride, stream):
+        B = js[0].keys.shape[0]
+        hh = [(i, idx_of[s.layer_idx]) for i, s in enumerate(js) if s.layer_idx in hh_layers]
+        if hh:
+            rows = [r for _, r in hh]
+            zl = [js[i].zone_len for i, _ in hh]
+            direct = all(r[3] <= stride and r[3] == js[i].n_select and r[2] <= zl_i
+                         for (i, r), zl_i in zip(hh, zl))
+            if direct:  # rows 0 .. n_hh*B - 1 of the region, in table order
+                run_heavy_hitters(mgr, rows, region, stride, stream)
+            else:  # manager k > compress heavy_hitter_size, or a middle longer than the zone
+                kmax = max(r[3] for r in rows)
+                tmp = torch.empty((len(rows) * B, kmax), dtype=torch.int32,
+                                  device=js[0].keys.device)
+                run_heavy_hitters(mgr, rows, tmp.data_ptr(), kmax, stream)
+                reg = _region_view(region, len(js) * B, stride, js[0].keys.device)
+                for (i, r), zl_i in zip(hh, zl):
+                    n = js[i].n_select
+                    if n:
+                        reg[i * B:(i + 1) * B, :n] = tmp[i * B:(i + 1) * B, :n].clamp(0, zl_i - 1)
+        host = [(i, idx_of[s.layer_idx]) for i, s in enumerate(js)
+                if s.layer_idx not in hh_layers]
+        if any(x is not None for _, x in host):
+            reg = _region_view(region, len(js) * B, stride, js[0].keys.device)
+            for i, x in host:
+                if x is not None:
+                    reg[i * B:(i + 1) * B, :x.numel()] = x.to(torch.int32)
+    E.execute_shared([s for s, _ in jobs], out_list, fill)
+
+
+def _region_view(ptr, rows, stride, device):
+    """The int32 index region at device address `ptr` as a [rows, stride] tensor (it lives in a
+    workspace the caller keeps alive until the launch)."""
+    class _Mem:  # minimal __cuda_array_interface__ provider
+        __cuda_array_interface__ = dict(shape=(rows, stride), typestr="<i4", data=(ptr, False),
+                                        version=3, strides=None)
+    with torch.cuda.device(device):
+        return torch.as_tensor(_Mem(), device=device)
 
 
 def create_h2o_manager_from_model(model, **kwargs) -> H2OAttentionManager:

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define KVC_ABI_VERSION 2
+#define KVC_ABI_VERSION 3
 
 typedef struct ihipStream_t* kvc_stream_t; /* a hipStream_t; NULL = legacy default stream */
 
@@ -70,7 +70,18 @@ enum kvc_phase {
   KVC_PHASE_ALL = 7
 };
 enum kvc_flag {
-  KVC_FLAG_SPLIT_SELECT_GATHER = 1 /* SELECT writes the index region, then a GATHER kernel */
+  KVC_FLAG_SPLIT_SELECT_GATHER = 1, /* SELECT writes the index region, then a GATHER kernel    */
+  KVC_FLAG_SHARED_INDEX = 2         /* external_index: index row (layer*batch + b) serves every
+                                       head of (layer, b) -- h2o_attention's heavy hitters, one
+                                       index list per layer (h2o_attention.py:326-333)        */
+};
+/* Bits the kernels OR into *params.device_status (when not NULL).  The word is sticky: the
+ * library never clears it; the caller zeroes it and reads it after the stream has drained. */
+enum kvc_device_status {
+  KVC_DEV_SELECT_BOUNDS = 1, /* a selection row exceeded its kernel's zone capacity: that row's
+                                output is unspecified (never expected: kvc_launch picks kernels
+                                by the planned zone lengths)                                  */
+  KVC_DEV_INDEX_RANGE = 2    /* an external index lay outside its zone and was clamped        */
 };
 enum kvc_status {
   KVC_OK = 0,
@@ -118,8 +129,9 @@ typedef struct kvc_params {
   int32_t algo;           /* enum kvc_algo  */
   int32_t phases;         /* OR of enum kvc_phase */
   int32_t external_index; /* 1: GATHER reads indices the caller wrote into the index region */
-  int32_t flags;          /* OR of enum kvc_flag */
-  int32_t reserved;       /* 0 */
+  int32_t flags;          /* OR of enum kvc_flag (other bits: KVC_E_ARG) */
+  int32_t reserved;       /* must be 0 (else KVC_E_ARG) */
+  uint32_t* device_status;/* optional device word for enum kvc_device_status bits (or NULL) */
 } kvc_params_t;
 
 typedef struct kvc_plan_info {
@@ -152,6 +164,68 @@ int kvc_launch(const kvc_params_t* params, const kvc_layer_t* layers, int num_la
 /* Convenience: kvc_plan + kvc_launch.  `layers` is updated in place. */
 int kvc_compress(const kvc_params_t* params, kvc_layer_t* layers, int num_layers,
                  void* workspace, size_t workspace_bytes, kvc_stream_t stream);
+
+
+/* ---------------------------------------------------------------------------------------------
+ * h2o_attention heavy hitters (reference: kvcompress/methods/h2o_attention.py).  The reference's
+ * H2OAttentionManager keeps per layer an accumulated attention tensor acc [B,H,len]:
+ *   update_attention_scores (:84-153)  acc = (acc*decay, zero-extended | zeros) + attn.sum(dim=2)
+ *   get_heavy_hitter_indices (:156-213) top-k of acc[:, :, m0:m1].sum(dim=1), sorted ascending
+ * Both sums follow torch's CPU reduction order (aten cascade_sum: four-level cascade per column,
+ * four interleaved lanes -- row_sum -- for the columns the SIMD loop leaves over, which depend on
+ * the reference process's thread chunks: col_chunk below); the top-k is the reference-exact
+ * std::nth_element / std::partial_sort set (KVC_ALGO_TOPK, descending).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct kvc_attn_params {
+  int32_t dtype;        /* enum kvc_dtype of attn / acc */
+  int32_t batch;
+  int32_t heads;
+  int32_t vec_bytes;    /* SIMD width of the reference's CPU sum kernel: 32 on x86 (sum_stub has
+                           no AVX512 variant) */
+  float decay;          /* decay_factor as the fp32 value torch multiplies by (:136, :146) */
+  int32_t flags;        /* 0 */
+  uint32_t* device_status; /* optional, as kvc_params_t */
+} kvc_attn_params_t;
+
+/* One layer of update_attention_scores (:100-154). */
+typedef struct kvc_attn_layer {
+  const void* attn;       /* [batch, heads, q_len, key_len], last dim contiguous */
+  int64_t attn_stride[3]; /* element strides of batch, heads, q */
+  const void* acc_old;    /* [batch, heads, old_len] contiguous (NULL when old_len == 0) */
+  void* acc_new;          /* [batch, heads, key_len] contiguous, written */
+  int32_t q_len;          /* >= 1 */
+  int32_t key_len;        /* >= 1 */
+  int32_t old_len;        /* 0: first update or reset (:118-123, :138-144); else <= key_len:
+                             columns [0, old_len) carry acc_old * decay (:129-137, :145-146) */
+  int32_t col_chunk;      /* columns per reference thread chunk of the q-sum; 0 = one chunk */
+} kvc_attn_layer_t;
+
+/* One layer of get_heavy_hitter_indices (:183-213). */
+typedef struct kvc_hh_layer {
+  const void* acc;        /* [batch, heads, acc_len] contiguous */
+  int32_t acc_len;
+  int32_t zone_start;     /* middle_start (:187) */
+  int32_t zone_len;       /* middle_end - middle_start >= 1 (:188, :205) */
+  int32_t n_select;       /* min(heavy_hitter_size, zone_len) (:206) */
+  int32_t col_chunk;      /* columns per reference thread chunk of the head sum; 0 = one */
+  int32_t reserved;       /* 0 */
+} kvc_hh_layer_t;
+
+/* acc_new of every layer (one kernel per chunk of layers). */
+int kvc_attn_accumulate(const kvc_attn_params_t* params, const kvc_attn_layer_t* layers,
+                        int num_layers, kvc_stream_t stream);
+
+/* Workspace kvc_heavy_hitters needs for this table. */
+int kvc_hh_workspace(const kvc_attn_params_t* params, const kvc_hh_layer_t* layers,
+                     int num_layers, size_t* bytes);
+
+/* Heavy hitters of every layer: row (layer*batch + b) of out_idx (int32, row stride
+ * out_row_stride >= max n_select) receives the n_select ascending zone-local indices of
+ * torch.topk(head_sum, n_select) (:198-211).  With out_idx = the index region of a
+ * KVC_FLAG_SHARED_INDEX gather plan, kvc_launch then compacts K/V (:305-361). */
+int kvc_heavy_hitters(const kvc_attn_params_t* params, const kvc_hh_layer_t* layers,
+                      int num_layers, int32_t* out_idx, int64_t out_row_stride, void* workspace,
+                      size_t workspace_bytes, kvc_stream_t stream);
 
 #ifdef __cplusplus
 }

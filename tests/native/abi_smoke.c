@@ -79,6 +79,12 @@ static int plan_checks(void) {
   CHECK(kvc_plan(&p, &l, 1, &info) == KVC_E_ARG, "n_select > zone rejected");
   l.n_select = 512;
   CHECK(kvc_launch(&p, &l, 1, NULL, 0, NULL) == KVC_E_WORKSPACE, "missing workspace rejected");
+  p.flags = 4;
+  CHECK(kvc_plan(&p, &l, 1, &info) == KVC_E_ARG, "unknown flag bit rejected");
+  p.flags = 0;
+  p.reserved = 1;
+  CHECK(kvc_plan(&p, &l, 1, &info) == KVC_E_ARG, "non-zero reserved field rejected");
+  p.reserved = 0;
   CHECK(strcmp(kvc_status_string(KVC_E_ALIGN), "pointer or stride not 16-byte aligned") == 0,
         "status string");
   printf("abi_smoke plan: ok\n");

@@ -29,9 +29,11 @@ def test_library_exports_every_declared_symbol():
 def test_struct_layout():
     L = N.lib()
     assert L.kvc_layer_struct_size() == N.LAYER_DTYPE.itemsize == 136
-    assert ctypes.sizeof(N.Params) == 40
+    assert ctypes.sizeof(N.Params) == 48
     assert ctypes.sizeof(N.PlanInfo) == 64
-    assert L.kvc_version() == N.ABI_VERSION == 2
+    assert ctypes.sizeof(N.AttnParams) == 32
+    assert N.ATTN_LAYER_DTYPE.itemsize == 64 and N.HH_LAYER_DTYPE.itemsize == 32
+    assert L.kvc_version() == N.ABI_VERSION == 3
     assert L.kvc_max_zone_len() == 1 << 24
 
 
@@ -39,7 +41,7 @@ def test_integration_stub_matches_abi():
     """The ctypes stub INTEGRATION.md offers a maintainer has kvc_params_t's fields, in order,
     and the layer layout of _native (which is checked against the library above)."""
     doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
-    m = re.search(r"class Params\(ctypes\.Structure\):.*?\((.*?)\)\]", doc, flags=re.S)
+    m = re.search(r"class Params\(ctypes\.Structure\):.*?\n(.*?)\nlib\.", doc, flags=re.S)
     names = re.findall(r'"(\w+)"', m.group(1))
     assert names == [f[0] for f in N.Params._fields_]
     layer = re.search(r"LAYER = np\.dtype\(\[(.*?)\]\)", doc, flags=re.S).group(1)
@@ -82,6 +84,7 @@ def test_plan_fills_prefix_fields_and_layout():
     (dict(head_dim=96), -3), (dict(head_dim=100), -3), (dict(batch=0), -1),
     (dict(order=3), -1), (dict(algo=9), -1)])
 def test_plan_rejects_bad_params(bad, code):
+    """(flags, reserved and device_status are covered by test_plan_rejects_unknown_flags)"""
     table = np.array([_layer(100, 0, 100, 10)], dtype=N.LAYER_DTYPE)
     rc, _ = N.plan(_params(**bad), table)
     assert rc == code
@@ -164,3 +167,61 @@ def test_launch_revalidates_against_plan():
     assert rc == 0
     table["unit0"] = 7  # tampered plan fields are rejected before any HIP call
     assert N.launch(_params(), table, 0, 0, 0) == -1
+
+
+def test_plan_rejects_unknown_flags():
+    """Unknown flag bits and a non-zero reserved field are refused, not ignored (a future flag
+    must not be silently dropped by this library); SHARED_INDEX needs external indices."""
+    table = np.array([_layer(100, 0, 100, 10)], dtype=N.LAYER_DTYPE)
+    assert N.plan(_params(flags=N.FLAG_SPLIT_SELECT_GATHER), table.copy())[0] == 0
+    assert N.plan(_params(flags=4), table.copy())[0] == -1
+    assert N.plan(_params(flags=1 << 30), table.copy())[0] == -1
+    assert N.plan(_params(reserved=1), table.copy())[0] == -1
+    assert N.plan(_params(flags=N.FLAG_SHARED_INDEX), table.copy())[0] == -1
+    assert N.plan(_params(flags=N.FLAG_SHARED_INDEX, external_index=1,
+                          phases=N.PHASE_GATHER), table.copy())[0] == 0
+
+
+def _attn_params(**kw):
+    d = dict(dtype=N.KVC_BF16, batch=1, heads=32, vec_bytes=32, decay=0.9, flags=0)
+    d.update(kw)
+    return N.AttnParams(**d)
+
+
+def test_heavy_hitter_workspace_and_validation():
+    """kvc_hh_workspace: head-summed rows [layers*batch, round_up(max zone, 64)] of dtype, plus
+    global selection scratch for zones longer than 16384; bad tables are refused."""
+    t = np.zeros(2, dtype=N.HH_LAYER_DTYPE)
+    t[0] = (4096, 2100, 4, 1652, 64, 0, 0)
+    t[1] = (4096, 600, 4, 152, 64, 0, 0)
+    rc, n = N.hh_workspace(_attn_params(), t)
+    assert rc == 0 and n == -(-(2 * 1664 * 2) // 256) * 256
+    rc, n4 = N.hh_workspace(_attn_params(dtype=N.KVC_F32), t)
+    assert rc == 0 and n4 == -(-(2 * 1664 * 4) // 256) * 256
+    long_ = t.copy()
+    long_[0]["acc_len"], long_[0]["zone_len"] = 40000, 39000
+    rc, nl = N.hh_workspace(_attn_params(), long_)
+    assert rc == 0 and nl > 2 * 39040 * 2 + 2 * 39040 * 4
+    for field, val in (("zone_len", 2097), ("n_select", 1653), ("zone_start", -1),
+                       ("reserved", 1), ("col_chunk", -2)):
+        bad = t.copy()
+        bad[0][field] = val
+        assert N.hh_workspace(_attn_params(), bad)[0] == -1, field
+    assert N.hh_workspace(_attn_params(vec_bytes=24), t)[0] == -1
+    assert N.hh_workspace(_attn_params(flags=1), t)[0] == -1
+    assert N.hh_workspace(_attn_params(dtype=9), t)[0] == -2
+
+
+def test_attn_accumulate_validates_before_launching():
+    t = np.zeros(1, dtype=N.ATTN_LAYER_DTYPE)
+    t[0] = (4096, (32 * 7 * 100, 7 * 100, 100), 0, 8192, 7, 100, 0, 0)
+    bad = t.copy()
+    bad[0]["old_len"] = 101  # more carried columns than the new key length
+    assert N.attn_accumulate(_attn_params(), bad, 0) == -1
+    bad = t.copy()
+    bad[0]["old_len"] = 50  # carried columns without acc_old
+    assert N.attn_accumulate(_attn_params(), bad, 0) == -1
+    bad = t.copy()
+    bad[0]["q_len"] = 0
+    assert N.attn_accumulate(_attn_params(), bad, 0) == -1
+    assert N.attn_accumulate(_attn_params(batch=0), t, 0) == -1

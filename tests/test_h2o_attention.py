@@ -40,17 +40,36 @@ def _drive(device):
     return kv, mgr, atts
 
 
+def test_oracle_manager_matches_reference_dyadic_golden():
+    """The CPU restatement (oracle/h2o_oracle.py) on the round-1 dyadic fixture."""
+    from oracle import h2o_oracle as HO
+    S = G.LENS[-1]
+    mgr = HO.H2OManager(decay_factor=0.5, **G.KW)
+    for step, key_len in enumerate(G.LENS[:-1]):
+        mgr.update_attention_scores(tuple(None if li == 2 else G.attention(step, li, key_len).numpy()
+                                          for li in range(G.L)))
+    mgr.update_attention_scores(tuple(None if li == 2 else G.attention(9, li, S).numpy()
+                                      for li in range(G.L)))
+    for li in range(G.L):
+        if f"acc_{li}" in GOLD:
+            np.testing.assert_array_equal(mgr.acc[li], GOLD[f"acc_{li}"])
+        else:
+            assert li not in mgr.acc
+        np.testing.assert_array_equal(mgr.get_heavy_hitter_indices(li, S), GOLD[f"idx_{li}"])
+
+
+@pytest.mark.gpu
 def test_manager_state_and_heavy_hitters_match_reference():
-    from kvcompress.methods.h2o_attention import h2o_attention_compress  # noqa: F401
-    kv, mgr, atts = _drive("cpu")
+    kv, mgr, atts = _drive("cuda:0")
     mgr.update_attention_scores(atts, skip_layers=[])
     S = G.LENS[-1]
     for li in range(G.L):
         if f"acc_{li}" in GOLD:
-            np.testing.assert_array_equal(mgr.accumulated_attention[li].numpy(), GOLD[f"acc_{li}"])
+            np.testing.assert_array_equal(mgr.accumulated_attention[li].cpu().numpy(),
+                                          GOLD[f"acc_{li}"])
         else:
             assert li not in mgr.accumulated_attention
-        np.testing.assert_array_equal(mgr.get_heavy_hitter_indices(li, S).numpy(),
+        np.testing.assert_array_equal(mgr.get_heavy_hitter_indices(li, S).cpu().numpy(),
                                       GOLD[f"idx_{li}"])
 
 
@@ -63,11 +82,16 @@ def test_registry_and_exports():
     assert get_compress_fn("h2o_attention") is h2o_attention_compress
 
 
-def test_cpu_tensors_raise_when_compressing():
-    from kvcompress.methods.h2o_attention import h2o_attention_compress
-    kv, mgr, atts = _drive("cpu")
+def test_cpu_tensors_raise():
+    """No CPU path: CPU attention (the manager's sums) and CPU K/V (the compaction) raise."""
+    from kvcompress.methods.h2o_attention import H2OAttentionManager, h2o_attention_compress
+    mgr = H2OAttentionManager(decay_factor=0.5, num_layers=G.L, num_heads=G.H, **G.KW)
     with pytest.raises(RuntimeError, match="ROCm GPU tensors only"):
-        h2o_attention_compress(kv, attention_scores=atts, h2o_manager=mgr, **G.KW)
+        mgr.update_attention_scores((G.attention(0, 0, 600),))
+    S = G.LENS[-1]
+    kv = [(torch.zeros(1, G.H, S, G.D), torch.zeros(1, G.H, S, G.D))]
+    with pytest.raises(RuntimeError, match="ROCm GPU tensors only"):
+        h2o_attention_compress(kv, **G.KW)
 
 
 @pytest.mark.gpu

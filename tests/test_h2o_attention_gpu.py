@@ -1,0 +1,165 @@
+"""h2o_attention's heavy-hitter scoring on the HIP engine vs the CPU reference (GPU tests).
+
+* the unmodified reference's outputs on tie-heavy, non-dyadic attention
+  (tests/golden/h2o_attention_ties.json): every layer's accumulated-attention bytes after every
+  step, the heavy-hitter indices and the compressed K/V, in fp32 / bf16 / fp16;
+* torch's own CPU ops (the reference's arithmetic) on random attention, across shapes and
+  thread counts: the engine's q-sum / decay / head-sum / top-k against torch CPU.
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+import h2o_inputs  # noqa: E402
+import prng  # noqa: E402
+from gen_h2o_attention_ties import att_seed, kv_seed  # noqa: E402
+from gpu_util import to_dev, to_np  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+GOLD = json.load(open(os.path.join(HERE, "golden", "h2o_attention_ties.json")))
+
+
+def sha(a):
+    a = np.ascontiguousarray(a)
+    return hashlib.sha256(str(a.shape).encode() + a.tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16", "fp16"])
+@pytest.mark.parametrize("si", [0, 1])
+def test_engine_replays_reference_tie_goldens(si, dt):
+    from kvcompress.methods.h2o_attention import H2OAttentionManager, h2o_attention_compress
+    sc = GOLD["scenarios"][si]
+    H, D, L = GOLD["H"], GOLD["D"], GOLD["layers"]
+    mgr = H2OAttentionManager(decay_factor=sc["decay"], num_layers=L, num_heads=H, **sc["kw"])
+    mgr.reduction_threads = GOLD["threads"]  # the generating process's torch threads
+    recs = GOLD["results"][f"{sc['name']}/{dt}"]
+    for st, step in enumerate(sc["steps"]):
+        k = step["k"] if step["op"] == "update" else step["S"]
+        atts = tuple(to_dev(h2o_inputs.attention(att_seed(si, st, li), H, step["q"], k, dt))
+                     if step["att"][li] else None for li in range(L))
+        rec = recs[st]
+        if step["op"] == "update":
+            mgr.update_attention_scores(atts, skip_layers=step["skip"])
+            S = k
+        else:
+            S = step["S"]
+            kv = [(to_dev(prng.gen_keys(kv_seed(si, st, li), (1, H, S, D), dt)),
+                   to_dev(prng.gen_values(kv_seed(si, st, li), (1, H, S, D), dt)))
+                  for li in range(L)]
+            out = h2o_attention_compress(list(kv), attention_scores=atts, h2o_manager=mgr,
+                                         skip_layers=step["skip"], **sc["kw"])
+            for li in range(L):
+                assert out[li][0].shape[2] == rec["n_out"][li], (st, li)
+                assert sha(to_np(out[li][0])) == rec["k"][li], ("K", st, li)
+                assert sha(to_np(out[li][1])) == rec["v"][li], ("V", st, li)
+        for li in range(L):
+            acc = mgr.accumulated_attention.get(li)
+            assert (None if acc is None else sha(to_np(acc))) == rec["acc"][li], ("acc", st, li)
+            got = mgr.get_heavy_hitter_indices(li, S)
+            assert got.cpu().tolist() == rec["idx"][li], ("idx", st, li)
+            if acc is not None and len(rec["idx"][li]):
+                assert got.device == acc.device and got.dtype == torch.int64
+    from kvcompress import _engine
+    assert _engine.device_status(0) == 0
+
+
+TORCH_DT = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}
+
+
+def _tie_attention(rng, shape, levels=4):
+    """Softmax rows over a few distinct logits (ties within and across heads), fp32."""
+    logits = rng.integers(0, levels, size=shape).astype(np.float32) * np.float32(0.7)
+    x = torch.from_numpy(logits).softmax(dim=-1)
+    return x
+
+
+@pytest.mark.parametrize("threads", [1, 8, 16, 33])
+@pytest.mark.parametrize("dt", ["fp32", "bf16", "fp16"])
+def test_engine_matches_torch_cpu_ops(threads, dt):
+    """update_attention_scores over three steps (first, extend, equal, reset) and
+    get_heavy_hitter_indices against the reference's arithmetic executed by torch on the CPU with
+    `threads` threads: attn.sum(dim=2), acc * decay, cat / zeros, acc + imp, head sum, topk."""
+    from kvcompress.methods.h2o_attention import H2OAttentionManager
+    rng = np.random.default_rng(threads)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        for B, H, steps, hh in [(1, 32, [(37, 1500), (1, 1501), (3, 1501), (1, 700)], 64),
+                                (1, 8, [(300, 2000), (1, 2001)], 16),
+                                (1, 4, [(5, 100), (17, 120)], 8),
+                                (1, 1, [(2, 3000), (1, 3001)], 32),
+                                (2, 16, [(9, 1100), (1, 1101)], 40)]:
+            mgr = H2OAttentionManager(start_size=4, heavy_hitter_size=hh, recent_size=50,
+                                      decay_factor=0.9)
+            mgr.reduction_threads = threads
+            acc_ref = None
+            for q, k in steps:
+                attn = _tie_attention(rng, (B, H, q, k)).to(TORCH_DT[dt])
+                mgr.update_attention_scores((attn.to("cuda:0"),))
+                imp = attn.sum(dim=2)  # the reference's ops (h2o_attention.py:116-151), CPU
+                if acc_ref is None or acc_ref.size(-1) > k:
+                    acc_ref = torch.zeros(B, H, k, dtype=attn.dtype)
+                elif acc_ref.size(-1) < k:
+                    acc_ref = torch.cat([acc_ref * 0.9, torch.zeros(B, H, k - acc_ref.size(-1),
+                                                                    dtype=attn.dtype)], dim=-1)
+                else:
+                    acc_ref = acc_ref * 0.9
+                acc_ref = acc_ref + imp
+                got = mgr.accumulated_attention[0]
+                assert np.array_equal(to_np(got).view(np.uint8), to_np(acc_ref).view(np.uint8)), \
+                    (B, H, q, k)
+                m1 = k - 50
+                agg = acc_ref[:, :, 4:m1].sum(dim=1)
+                if B == 1:
+                    agg = agg.squeeze(0)
+                _, top = torch.topk(agg, min(hh, m1 - 4), dim=-1)
+                top, _ = torch.sort(top, dim=-1)
+                assert mgr.get_heavy_hitter_indices(0, k).cpu().tolist() == top.tolist(), \
+                    (B, H, q, k)
+    finally:
+        torch.set_num_threads(prev)
+
+
+def test_shared_index_gather_and_index_range_status():
+    """C-ABI level: a KVC_FLAG_SHARED_INDEX gather reads row (layer*B + b) for every head, and an
+    external index outside its zone is clamped AND reported through params.device_status."""
+    from kvcompress import _native as N
+    H, S, D = 4, 256, 64
+    k = torch.arange(H * S * D, dtype=torch.float32, device="cuda:0").reshape(1, H, S, D)
+    v = -k
+    n_sel = 3
+    ko = torch.empty(1, H, n_sel, D, device="cuda:0")
+    vo = torch.empty_like(ko)
+    t = np.zeros(1, dtype=N.LAYER_DTYPE)
+    t[0] = (k.data_ptr(), v.data_ptr(), ko.data_ptr(), vo.data_ptr(), (H * S * D, S * D, D),
+            (H * S * D, S * D, D), S, 10, 100, n_sel, 0, 0, 0, 0, 0, 0, 0, 0, 0)
+    status = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    p = N.Params(dtype=N.KVC_F32, batch=1, heads=H, head_dim=D, order=0, algo=0,
+                 phases=N.PHASE_GATHER, external_index=1, flags=N.FLAG_SHARED_INDEX,
+                 device_status=status.data_ptr())
+    rc, info = N.plan(p, t)
+    assert rc == 0
+    ws = torch.zeros(int(info.workspace_bytes), dtype=torch.uint8, device="cuda:0")
+    idx = ws[info.index_offset:info.index_offset + 4 * n_sel].view(torch.int32)
+    idx.copy_(torch.tensor([5, 7, 99], dtype=torch.int32))
+    rc = N.launch(p, t, ws.data_ptr(), int(info.workspace_bytes),
+                  torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    torch.cuda.synchronize()
+    want = torch.tensor([15, 17, 109], device="cuda:0")
+    assert torch.equal(ko, k[:, :, want]) and torch.equal(vo, v[:, :, want])
+    assert int(status.item()) == 0
+    idx.copy_(torch.tensor([5, 7, 100], dtype=torch.int32))  # zone_len 100: out of range
+    assert N.launch(p, t, ws.data_ptr(), int(info.workspace_bytes),
+                    torch.cuda.current_stream().cuda_stream) == 0
+    torch.cuda.synchronize()
+    assert int(status.item()) == N.DEV_INDEX_RANGE
+    assert torch.equal(ko, k[:, :, want])  # clamped to the zone's last row
