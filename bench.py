@@ -282,6 +282,21 @@ def capture_jobs(step):
     return seen
 
 
+def dump_first_layer(dirname, rank, layer0, layers, out):
+    """Test hook (--dump-layer): heads 0-1 of this rank's first layer -- inputs and the engine's
+    outputs -- as bit patterns in DIR/rank<r>.npz, for tests/test_bench_multirank.py to check
+    against the oracle.  Nothing here runs in the timed region."""
+    import numpy as np
+
+    def bits(t):
+        t = t[:, :2].contiguous().cpu()
+        return t.view(torch.int16).numpy() if t.element_size() == 2 else t.numpy()
+    os.makedirs(dirname, exist_ok=True)
+    (k, v), (ko, vo) = layers[0], out[0]
+    np.savez(os.path.join(dirname, f"rank{rank}.npz"), k=bits(k), v=bits(v), k_out=bits(ko),
+             v_out=bits(vo), layer=layer0, dtype=str(k.dtype))
+
+
 def _free_port():
     sock = socket.socket()
     sock.bind(("127.0.0.1", 0))
@@ -335,6 +350,11 @@ def main():
                     help="architecture of the random-init model of the PPL-delta leg")
     ap.add_argument("--dry-run", action="store_true",
                     help="harness check on CPU: gloo, stand-in step, no engine, no GPU")
+    ap.add_argument("--same-device", action="store_true",
+                    help="test only: every rank uses cuda:0 (a multi-rank run on a 1-GPU box)")
+    ap.add_argument("--dump-layer", default=None, metavar="DIR",
+                    help="test only: after the timed region each rank writes its first layer's "
+                         "K/V inputs and outputs (heads 0-1) to DIR/rank<r>.npz")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -346,6 +366,7 @@ def main():
         dev = torch.device("cpu")
         sync = lambda: None  # noqa: E731
     else:
+        local = 0 if args.same_device else local
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         sync = torch.cuda.synchronize
@@ -463,6 +484,9 @@ def main():
             "tokens_evicted_per_sec": None,
         }
         ev = sum(kv[0].size(2) for kv in layers) - sum(kv[0].size(2) for kv in step())
+    if args.dump_layer and not args.dry_run:
+        dump_first_layer(args.dump_layer, rank, l0, layers, step())
+    if rank == 0:
         res["tokens_evicted_per_sec"] = ev * world * args.steps / elapsed
         if args.dry_run:
             res["dry_run"] = True

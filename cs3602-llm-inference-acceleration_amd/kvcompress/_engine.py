@@ -46,16 +46,34 @@ class HipEvent:
     """A timing event created with hipEventDisableSystemFence, recorded on a raw HIP stream:
     recording it does not write back / invalidate caches the way torch.cuda.Event's default
     events do (measured: split launches with torch events cost the headline step 1.5-2.3 %,
-    tools/timer_overhead.py).  Uses the HIP runtime instance torch loaded (same soname)."""
+    tools/timer_overhead.py).  Uses the HIP runtime instance torch has loaded (found in the
+    process's memory map, whatever its soname); PhaseTimer falls back to torch.cuda.Event when
+    it cannot be found."""
 
     _hip = None
     DISABLE_SYSTEM_FENCE = 0x20000000
+
+    @staticmethod
+    def loaded_runtime():
+        """Path of the libamdhip64 this process has mapped (torch's), or None."""
+        try:
+            with open("/proc/self/maps") as f:
+                for line in f:
+                    path = line.split()[-1]
+                    if "/libamdhip64.so" in path:
+                        return path
+        except OSError:
+            pass
+        return None
 
     @classmethod
     def _lib(cls):
         if cls._hip is None:
             import ctypes
-            h = ctypes.CDLL("libamdhip64.so.7")
+            path = cls.loaded_runtime()
+            if path is None:
+                raise OSError("the HIP runtime is not loaded in this process")
+            h = ctypes.CDLL(path)
             h.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
             h.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
             h.hipEventSynchronize.argtypes = [ctypes.c_void_p]
@@ -80,7 +98,9 @@ class HipEvent:
     def elapsed_time(self, end):
         import ctypes
         ms = ctypes.c_float()
-        self._lib().hipEventSynchronize(end._ev)
+        rc = self._lib().hipEventSynchronize(end._ev)
+        if rc != 0:
+            raise RuntimeError(f"hipEventSynchronize failed ({rc})")
         rc = self._lib().hipEventElapsedTime(ctypes.byref(ms), self._ev, end._ev)
         if rc != 0:
             raise RuntimeError(f"hipEventElapsedTime failed ({rc})")
@@ -107,7 +127,14 @@ class PhaseTimer:
         self.steps = steps or self.DEFAULT
         self.records = []
         self.workspaces = [] if keep_workspace else None  # (ws, info) of each launch (tools)
-        self.event = HipEvent if fenceless else (lambda: torch.cuda.Event(enable_timing=True))
+        torch_event = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+        if fenceless:
+            try:
+                HipEvent._lib()
+            except OSError:
+                fenceless = False  # no mapped HIP runtime to call: torch's events
+        self.fenceless = fenceless
+        self.event = HipEvent if fenceless else torch_event
 
     def durations_ms(self):
         torch.cuda.synchronize()
@@ -196,8 +223,11 @@ def _one_plain_group(jobs):
                 not (k.is_contiguous() and v.is_contiguous()) or k.get_device() != dev or
                 v.get_device() != dev):
             return None
-        kps.append(k.data_ptr())
-        vps.append(v.data_ptr())
+        kp, vp = k.data_ptr(), v.data_ptr()
+        if (kp | vp) & 15:  # e.g. a contiguous view at an odd offset: the general path copies
+            return None
+        kps.append(kp)
+        vps.append(vp)
         segs.append((ks[2], j.zone_start, j.zone_len, j.n_select, j.sink_len, j.tail_start,
                      j.tail_len, j.pool_kernel, j.score_mode))
     return dev, dt, B, H, D, kps, vps, segs
@@ -250,11 +280,19 @@ class _PlanCache:
     zero), kvc_plan_info, the workspace and the params.  A workspace is reused only by calls on
     the SAME stream, which are ordered behind the kernels that used it before.  Calls with
     caller-provided indices (strategy="random") are not cached: their workspace holds per-call
-    data."""
+    data.
 
-    def __init__(self, capacity=8):
+    Memory: a shape is cached on its SECOND sighting (a one-off call -- a prefill, a decode step
+    whose S grows every token -- keeps no workspace), at most `capacity` entries and `max_bytes`
+    of workspace are held (least recently used first out), and clear() releases them all."""
+
+    def __init__(self, capacity=8, max_bytes=1 << 30, seen_capacity=64):
         self.capacity = capacity
+        self.max_bytes = max_bytes
+        self.seen_capacity = seen_capacity
         self.entries = {}
+        self.seen = {}
+        self.bytes = 0
 
     def get(self, key):
         e = self.entries.get(key)
@@ -263,13 +301,30 @@ class _PlanCache:
             self.entries[key] = e
         return e
 
-    def put(self, key, entry):
-        if len(self.entries) >= self.capacity:
-            del self.entries[next(iter(self.entries))]
-        self.entries[key] = entry
+    def admit(self, key):
+        """True on a key's second sighting (the caller then plans and put()s it)."""
+        if key in self.seen:
+            del self.seen[key]
+            return True
+        if len(self.seen) >= self.seen_capacity:
+            del self.seen[next(iter(self.seen))]
+        self.seen[key] = None
+        return False
+
+    def put(self, key, entry, nbytes):
+        if nbytes > self.max_bytes:
+            return
+        while self.entries and (len(self.entries) >= self.capacity or
+                                self.bytes + nbytes > self.max_bytes):
+            old = self.entries.pop(next(iter(self.entries)))
+            self.bytes -= old[-1]
+        self.entries[key] = entry + (nbytes,)
+        self.bytes += nbytes
 
     def clear(self):
         self.entries.clear()
+        self.seen.clear()
+        self.bytes = 0
 
 
 plan_cache = _PlanCache()
@@ -343,8 +398,9 @@ def _run_plain(device, dtype, B, H, D, kps, vps, segs, js, out_list, order, algo
             if entry is None:  # rejected by kvc_plan (e.g. misaligned): general path reports
                 _run_general(device, dtype, B, H, D, js, out_list, order, algo, False, stream)
                 return
-            plan_cache.put(key, entry)
-        tmpl, info, ws, p, n_outs = entry
+            if plan_cache.admit(key):
+                plan_cache.put(key, entry, int(entry[2].numel()))
+        tmpl, info, ws, p, n_outs = entry[:5]
         kos, vos, kops, vops = _outputs(device, dtype, B, H, D, n_outs)
         table = tmpl.copy()
         table["k"] = kps

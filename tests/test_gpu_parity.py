@@ -399,3 +399,23 @@ def test_layer_sharded_calls_match_unsharded_oracle(name, kw):
     assert len(got) == L
     for li, ((ko, vo), (rk, rv, _)) in enumerate(zip(got, ref)):
         assert np.array_equal(to_np(ko), rk) and np.array_equal(to_np(vo), rv), (name, li)
+
+
+def test_misaligned_contiguous_views_take_the_general_path():
+    """A contiguous K/V view at an odd element offset into a flat buffer (not 16-B aligned): the
+    one-pass fast path declines it and the general path's aligned copy computes it exactly."""
+    from kvcompress.methods import fix_size_l2_compress
+    shape = (1, 4, 300, 64)
+    kn = prng.gen_keys(4242, shape, "bf16", "few")
+    vn = prng.gen_values(4242, shape, "bf16")
+    n = kn.size
+    flat_k = torch.empty(n + 3, dtype=torch.bfloat16, device="cuda:0")
+    flat_v = torch.empty(n + 3, dtype=torch.bfloat16, device="cuda:0")
+    k = flat_k[3:].view(shape)
+    v = flat_v[3:].view(shape)
+    k.copy_(to_dev(kn))
+    v.copy_(to_dev(vn))
+    assert k.is_contiguous() and k.data_ptr() % 16 != 0
+    out = fix_size_l2_compress([(k, v)], fix_kv_size=100, skip_layers=[])
+    rk, rv, _ = oracle.fix_size_l2_compress([(kn, vn)], fix_kv_size=100, skip_layers=[])[0]
+    assert np.array_equal(to_np(out[0][0]), rk) and np.array_equal(to_np(out[0][1]), rv)
