@@ -183,7 +183,9 @@ def _prep(t):
         return t  # the common case, one C call
     ok = (t.stride(3) == 1 and t.data_ptr() % 16 == 0 and
           all((t.stride(d) * es) % 16 == 0 or t.size(d) == 1 for d in range(3)))
-    return t if ok else t.contiguous()
+    # a fresh allocation is aligned (.contiguous() would return a contiguous-but-misaligned view
+    # -- e.g. one at an odd offset into a flat buffer -- as it is)
+    return t if ok else t.clone(memory_format=torch.contiguous_format)
 
 
 def execute(jobs: List[Segments], out_list: list, order: int, algo: int):
