@@ -298,10 +298,12 @@ class _PlanCache:
 
     def get(self, key):
         e = self.entries.get(key)
-        if e is not None and len(self.entries) > 1:  # most recently used last
+        if e is None:
+            return None
+        if len(self.entries) > 1:  # most recently used last
             del self.entries[key]
             self.entries[key] = e
-        return e
+        return e[0]
 
     def admit(self, key):
         """True on a key's second sighting (the caller then plans and put()s it)."""
@@ -319,8 +321,8 @@ class _PlanCache:
         while self.entries and (len(self.entries) >= self.capacity or
                                 self.bytes + nbytes > self.max_bytes):
             old = self.entries.pop(next(iter(self.entries)))
-            self.bytes -= old[-1]
-        self.entries[key] = entry + (nbytes,)
+            self.bytes -= old[1]
+        self.entries[key] = (entry, nbytes)
         self.bytes += nbytes
 
     def clear(self):
@@ -402,7 +404,10 @@ def _run_plain(device, dtype, B, H, D, kps, vps, segs, js, out_list, order, algo
                 return
             if plan_cache.admit(key):
                 plan_cache.put(key, entry, int(entry[2].numel()))
-        tmpl, info, ws, p, n_outs = entry[:5]
+        tmpl, info, ws, p, n_outs = entry
+        if _recording is not None:
+            _recording.append((stream.cuda_stream, tmpl, info, ws, p, n_outs,
+                               [j.layer_idx for j in js]))
         kos, vos, kops, vops = _outputs(device, dtype, B, H, D, n_outs)
         table = tmpl.copy()
         table["k"] = kps
@@ -417,6 +422,8 @@ def _run_plain(device, dtype, B, H, D, kps, vps, segs, js, out_list, order, algo
 
 
 def _run_group(device, dtype, B, H, D, js, out_list, order, algo):
+    if _recording is not None:
+        _recording.append(None)  # a general-path launch: this call shape is not replayable
     external = any(j.ext_index is not None for j in js)
     if external and not all(j.ext_index is not None or j.n_select == 0 for j in js):
         raise RuntimeError("mixed external / engine-selected layers in one group")
@@ -485,6 +492,8 @@ def execute_shared(jobs: List[Segments], out_list: list, fill):
     (KVC_FLAG_SHARED_INDEX: h2o_attention's heavy hitters, one index list per layer).  Per group,
     `fill(js, index_region_ptr, row_stride, stream)` writes row (i * B + b) of job i before the
     copy kernel is enqueued on the same stream."""
+    if _recording is not None:
+        _recording.append(None)
     groups = {}
     for j in jobs:
         B, H, _, D = _check_tensors(j)
@@ -517,3 +526,140 @@ def _run_general(device, dtype, B, H, D, js, out_list, order, algo, external, st
         _timer.workspaces.append((ws, info))
     for j, ko, vo in zip(js, kos, vos):
         out_list[j.layer_idx] = (ko, vo)
+
+
+# ---------------------------------------------------------------------------------------------
+# Call memo: repeated call shapes replayed by the native host path (csrc/kvc_host.cpp)
+# ---------------------------------------------------------------------------------------------
+_recording = None  # list while a call is being recorded: one entry per engine launch
+_host = None
+
+
+def host_module():
+    """kvc_host.so (built by __graft_entry__.build()), or None when it is not there -- calls then
+    take the method's Python path (same engine, same results, more host time per call)."""
+    global _host
+    if _host is None:
+        import importlib.util
+        import os
+        path = os.path.join(os.path.dirname(N.LIB_PATH), "kvc_host.so")
+        _host = False
+        if os.path.exists(path):
+            spec = importlib.util.spec_from_file_location("kvc_host", path)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            _host = mod
+    return _host or None
+
+
+def _freeze(x):
+    if isinstance(x, (list, tuple)):
+        return tuple(_freeze(y) for y in x)
+    if isinstance(x, (int, float, str, bool, type(None))):
+        return x
+    raise TypeError  # anything else (a manager object, a tensor): not memoised
+
+
+class _Replay:
+    __slots__ = ("actions", "table", "n_jobs", "n_outs", "params", "ws", "ws_bytes", "keep")
+
+
+def _record(kvl, out, launches):
+    """A _Replay of one recorded call, or None when the call is not replayable (a general-path
+    launch, more than one launch, or a layer that is neither passed through, a dim-2 slice of
+    its input, nor an engine output)."""
+    if len(launches) > 1 or any(x is None for x in launches):
+        return None
+    job_of = {}
+    rec = _Replay()
+    rec.table, rec.n_jobs, rec.n_outs, rec.params, rec.ws, rec.ws_bytes = 0, 0, [], None, None, 0
+    if launches:
+        _, tmpl, info, ws, p, n_outs, layer_ids = launches[0]
+        job_of = {li: j for j, li in enumerate(layer_ids)}
+        rec.table, rec.n_jobs = tmpl.ctypes.data, len(tmpl)
+        rec.n_outs, rec.params, rec.ws = [int(x) for x in n_outs], p, ws
+        rec.ws_bytes = int(info.workspace_bytes)
+        rec.keep = (tmpl, info, ws, p)
+    acts = np.zeros((len(kvl), 3), dtype=np.int64)
+    for i, (inp, res) in enumerate(zip(kvl, out)):
+        if res is inp:
+            continue
+        if i in job_of:
+            acts[i] = (2, job_of[i], 0)
+            continue
+        k, v = inp
+        rk, rv = res
+        st = k.stride(2)
+        if (rk.untyped_storage().data_ptr() != k.untyped_storage().data_ptr() or
+                rk.shape[:2] != k.shape[:2] or rk.shape[3] != k.shape[3] or
+                rk.stride() != k.stride() or st == 0 or
+                (rk.storage_offset() - k.storage_offset()) % st):
+            return None
+        start = (rk.storage_offset() - k.storage_offset()) // st
+        if not (rv.shape == rk.shape and rv.stride() == v.stride() and
+                rv.storage_offset() - v.storage_offset() == start * v.stride(2)):
+            return None
+        acts[i] = (1, start, rk.shape[2])
+    rec.actions = acts
+    return rec
+
+
+call_memo = _PlanCache(capacity=16)
+memo_stats = {"replayed": 0, "recorded": 0}
+
+
+def memoized(fn):
+    """Wrap a compress function: a call shape seen before (same function, arguments, per-layer
+    shapes / dtype / device / stream) is replayed by kvc_host.run -- one C++ call that fills the
+    recorded launch's pointers, allocates the outputs and enqueues the kernels -- instead of
+    re-running the reference's per-layer branch logic in Python.  The first sightings run `fn`
+    itself; the second records what it did (per layer: passed through, sliced, or engine
+    output, and the engine launch's plan).  Results are identical either way."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrapper(past_key_values, *args, **kwargs):
+        global _recording
+        hm = host_module()
+        if hm is None or _timer is not None or _recording is not None:
+            return fn(past_key_values, *args, **kwargs)
+        from .utils import normalize_kv_cache
+        kvl = list(normalize_kv_cache(past_key_values))
+        sig = hm.scan(kvl)
+        if sig is None:
+            return fn(kvl, *args, **kwargs)
+        try:
+            key = (fn, _freeze(args), _freeze(sorted(kwargs.items())), split_select_gather,
+                   torch.cuda.current_stream(sig[4]).cuda_stream, sig)
+        except TypeError:
+            return fn(kvl, *args, **kwargs)
+        rec = call_memo.get(key)
+        if rec is not None:
+            memo_stats["replayed"] += 1
+            if rec.n_jobs and torch.cuda.current_device() != sig[4]:
+                with torch.cuda.device(sig[4]):
+                    return hm.run(kvl, rec.actions, rec.table, rec.n_jobs, rec.n_outs,
+                                  ctypes_addr(rec.params), rec.ws.data_ptr(), rec.ws_bytes,
+                                  key[4])
+            return hm.run(kvl, rec.actions, rec.table, rec.n_jobs, rec.n_outs,
+                          ctypes_addr(rec.params) if rec.n_jobs else 0,
+                          rec.ws.data_ptr() if rec.n_jobs else 0, rec.ws_bytes, key[4])
+        if not call_memo.admit(key):
+            return fn(kvl, *args, **kwargs)
+        _recording = []
+        try:
+            out = fn(kvl, *args, **kwargs)
+            launches = _recording
+        finally:
+            _recording = None
+        rec = _record(kvl, out, launches)
+        if rec is not None and all(l[0] == key[4] for l in launches):
+            call_memo.put(key, rec, rec.ws_bytes)
+            memo_stats["recorded"] += 1
+        return out
+    return wrapper
+
+
+def ctypes_addr(obj):
+    import ctypes
+    return ctypes.addressof(obj)

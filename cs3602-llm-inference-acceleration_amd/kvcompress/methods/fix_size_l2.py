@@ -13,6 +13,7 @@ from .. import _native as N
 from ..utils import layer_offset, normalize_kv_cache
 
 
+@E.memoized
 def fix_size_l2_compress(
     past_key_values,
     fix_kv_size: int = 1024,

@@ -12,6 +12,7 @@ from .. import _native as N
 from ..utils import layer_offset, normalize_kv_cache
 
 
+@E.memoized
 def h2o_l2_compress(
     past_key_values,
     start_size: int = 4,

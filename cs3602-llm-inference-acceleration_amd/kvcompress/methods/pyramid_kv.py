@@ -32,6 +32,7 @@ def pyramid_layer_sizes(num_layers, base_size=512, layer_decay=0.9, min_size=64,
     return sizes
 
 
+@E.memoized
 def pyramid_kv_compress(
     past_key_values,
     base_size: int = 512,

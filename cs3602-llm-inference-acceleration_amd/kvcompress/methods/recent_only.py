@@ -6,9 +6,11 @@ from typing import List, Tuple
 
 import torch
 
+from .. import _engine as E
 from ..utils import layer_offset, normalize_kv_cache
 
 
+@E.memoized
 def recent_only_compress(
     past_key_values,
     window_size: int = 512,

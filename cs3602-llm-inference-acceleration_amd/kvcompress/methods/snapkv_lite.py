@@ -13,6 +13,7 @@ from .. import _native as N
 from ..utils import layer_offset, normalize_kv_cache
 
 
+@E.memoized
 def snapkv_lite_compress(
     past_key_values,
     observation_window: int = 32,

@@ -28,6 +28,7 @@ def _sink_recent_jobs(past_key_values, start_size, recent_size, skip_layers, fit
     return jobs
 
 
+@E.memoized
 def streaming_llm_compress(
     past_key_values,
     start_size: int = 4,
@@ -45,6 +46,7 @@ def streaming_llm_compress(
     return past_key_values
 
 
+@E.memoized
 def evict_for_space(
     past_key_values,
     num_coming: int,
