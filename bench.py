@@ -43,6 +43,8 @@ WORKLOADS = {
                       16384, 128, "headline"),
     "fix512-s4096": ("fix_size_l2", dict(fix_kv_size=512, keep_ratio=0.0, strategy="keep_low"),
                      4096, 128, "cfg2 geometry of the north star ([1,32,S,128])"),
+    "fix512-s8192": ("fix_size_l2", dict(fix_kv_size=512, keep_ratio=0.0, strategy="keep_low"),
+                     8192, 128, "between the north star's two lengths"),
     "fix512-s4096-d80": ("fix_size_l2", dict(fix_kv_size=512, keep_ratio=0.0,
                                              strategy="keep_low"), 4096, 80, "cfg2, pythia-2.8b"),
     "streaming-s16384": ("streaming_llm", dict(start_size=4, recent_size=1020), 16384, 80,

@@ -35,12 +35,17 @@ constexpr int kScoreWaves = kScoreThreads / 64;
 constexpr int kSelThreads = 1024;
 constexpr int kSelWaves = kSelThreads / 64;
 // Zones of up to kSmallZone positions select with 512-thread workgroups and LDS sized by the
-// call's longest zone: all 1 024 rows of a 32-layer call are resident at once (4 per CU), and a
-// row's copy phase has 8 waves of loads in flight (256-thread rows: SELECT_GATHER 0.129 ms at
-// S = 4 096, 0.104 ms at S = 513; 512: 0.115 / 0.096).  Longer zones keep 1 024 threads (512
-// measured slower at 8 192 positions: 0.157 vs 0.147 ms).
+// call's longest zone, at most kSmallBudget bytes: four rows per CU (all 1 024 rows of a
+// 32-layer call resident at once), a row's copy phase with 8 waves of loads in flight
+// (256-thread rows: SELECT_GATHER 0.129 ms at S = 4 096, 0.104 ms at S = 513; 512: 0.115 /
+// 0.096).  Up to 8 192 positions the budget holds the bf16 / fp16 rows with rank windows
+// (profiles/r03_d_small_path_rows_per_cu_ab.jsonl, S = 8 192: 0.137 ms with 1 024-thread rows
+// two per CU, 0.148 ms with 512-thread rows three per CU and full tables, 0.1265 ms four per CU
+// with windows).  Longer zones keep 1 024 threads.
 constexpr int kSelThreadsSmall = 512;
-constexpr int kSmallZone = 4096;
+constexpr int kSmallZone = 8192;
+constexpr long kSmallBudget = 40448;  // 4 x (this + scalars) <= 160 KiB of LDS per CU
+constexpr long kBigBudget = 81408;    // 2 x (this + scalars) <= 160 KiB
 constexpr int kZoneMax = 16384;        // longest zone whose selection runs from LDS
 constexpr int kZoneMaxGlobal = 65536;  // longest zone of the u16-position global variant
 constexpr int kZoneMaxLong = 1 << 24;   // longest zone at all (u32 positions; global scratch)
@@ -329,14 +334,14 @@ struct SelScalars {
 __host__ __device__ constexpr size_t sel_bytes(int n_cap, int key_size, int cap) {
   return (size_t)n_cap * key_size + (size_t)n_cap * 2 + (size_t)(64 + cap + 8) * 2 * 2;
 }
-// Rank-window size for an n_cap-position LDS selection.  bf16 rows of up to 16 384 positions fit
-// two workgroups per CU (<= 80 KiB each, 160 KiB LDS per CU) when the tables hold fewer than the
-// n_cap/2 ranks a level can need; levels with more swaps take a second window.  fp32 keys (and
-// short zones) get full tables.
-__host__ __device__ constexpr int sel_cap(int n_cap, int key_size) {
+// Rank-window size for an n_cap-position LDS selection within `budget` bytes of arrays.  16-bit
+// keys fit the budget when the tables hold fewer than the n_cap/2 ranks a level can need; levels
+// with more swaps take further windows.  fp32 keys (whose snapkv scores use the tables as
+// scratch) and short zones get full tables.
+__host__ __device__ constexpr int sel_cap(int n_cap, int key_size, long budget) {
   const int full = n_cap / 2 + 1;
-  const long budget = 81408L - (long)n_cap * (key_size + 2) - 4L * 72;  // bytes for the tables
-  const int fit = budget > 0 ? (int)(budget / 4) : 0;
+  const long tables = budget - (long)n_cap * (key_size + 2) - 4L * 72;  // bytes for the tables
+  const int fit = tables > 0 ? (int)(tables / 4) : 0;
   return (key_size == 2 && fit < full && fit >= 1024) ? (fit & ~63) : full;
 }
 template <typename KeyT>
@@ -716,7 +721,9 @@ __device__ __forceinline__ void p2_window0(const KeyT* key, uint16_t* spos, uint
                                            int lane, int pos0, int wbeg, int J, int hi,
                                            uint32_t p, int ch, bool kge, bool kle, int rge1,
                                            int rle, int tot_le, int cap, int& nsw) {
-  constexpr int JB = JM < 8 ? JM : 8;  // keys in flight per lane (register budget: 64 VGPRs)
+  // keys in flight per lane (register budget: 64 VGPRs); 4 and 16 measured the same
+  // (profiles/r03_c_p2_keys_in_flight_ab.jsonl): the level is latency-, not issue-bound
+  constexpr int JB = JM < 8 ? JM : 8;
   const int t1 = tot_le + 1;
   unroll_for<0, JM / JB>([&](auto bc) {
     constexpr int j0 = decltype(bc)::value * JB;
@@ -964,7 +971,7 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
     acc[4] += (uint64_t)msw;
     if (NT > 64) acc[25] = (t1 - t0) | ((t2 - t1) << 20) | ((t3 - t2) << 40);  // level split
 #ifdef KVC_SNAP_STAMPS
-    if (false) {  // slots 26..29 hold the snapkv scoring stamps (tools/gpu_snapstamps.sh)
+    if (false) {  // slots 26..29 hold the snapkv scoring stamps (tools/select_stamps.py with SEL_SNAP_STAMPS)
 #else
     if (NT > 64 && JM == 16 && J == 16) {  // level 0 of a 16 384-position row (slots 26..29):
 #endif
@@ -1389,7 +1396,7 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
 // CU.  NT = 1 024 beyond, arrays in static LDS laid out for kZoneMax (compile-time addresses)
 // with rank windows of kSelCapBig: two rows per CU for bf16.
 template <typename KeyT>
-constexpr int kSelCapBig = sel_cap(kZoneMax, (int)sizeof(KeyT));
+constexpr int kSelCapBig = sel_cap(kZoneMax, (int)sizeof(KeyT), kBigBudget);
 template <typename KeyT>
 constexpr int kSelBytesBig = (int)sel_bytes(kZoneMax, (int)sizeof(KeyT), kSelCapBig<KeyT>);
 
@@ -2195,7 +2202,7 @@ static int launch_select(const LayerChunk& T, int cn, int BH, int dt, int order,
   }
   const int ks = (int)sizeof(KeyT);
   if (n_cap <= kSmallZone) {
-    const int cap = sel_cap(n_cap, ks);
+    const int cap = sel_cap(n_cap, ks, kSmallBudget);
     return launch_k(select_kernel<KC, kSelThreadsSmall>, rows_grid, dim3(kSelThreadsSmall),
                     sel_bytes(n_cap, ks, cap), s, T, BH, dt, order, algo, norms, nstride, idx,
                     istride, kWaveSeg, n_cap, cap, stamps, status);
@@ -2246,7 +2253,7 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
       const dim3 rows_grid((unsigned)(cn * BH));
       const int ks = (int)sizeof(KeyT);
       if (n_cap <= kSmallZone) {
-        const int cap = sel_cap(n_cap, ks);
+        const int cap = sel_cap(n_cap, ks, kSmallBudget);
         return launch_k(select_gather_kernel<KC, kSelThreadsSmall, NC>, rows_grid,
                         dim3(kSelThreadsSmall), sel_bytes(n_cap, ks, cap), s, T, H, BH, DT,
                         p->order, p->algo, norms, nstride, kWaveSeg, n_cap, cap, status);

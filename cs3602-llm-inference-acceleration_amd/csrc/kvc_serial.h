@@ -9,7 +9,8 @@
 //   std::__move_median_to_first, std::__insertion_sort / __unguarded_linear_insert,
 //   std::__adjust_heap, std::__push_heap, std::__make_heap, std::__pop_heap,
 //   std::__sort_heap, std::__heap_select.
-// tests/native/test_serial.cpp checks these against the real libstdc++ algorithms.
+// tests/native/select_model.cpp (run by tests/test_select_model.py) checks these, with the
+// kernel's own key mapping, against the real libstdc++ algorithms.
 #pragma once
 
 #include "kvc_common.h"

@@ -544,7 +544,9 @@ def host_module():
         import os
         path = os.path.join(os.path.dirname(N.LIB_PATH), "kvc_host.so")
         _host = False
-        if os.path.exists(path):
+        # kvc_host.so links the default libkvc.so: a swapped-in build (KVC_LIB, A/B runs) keeps
+        # every call on the ctypes path so that all launches use the same library
+        if os.path.exists(path) and os.path.basename(N.LIB_PATH) == "libkvc.so":
             spec = importlib.util.spec_from_file_location("kvc_host", path)
             mod = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(mod)

@@ -50,3 +50,28 @@ def test_reference_citations_in_range():
                         bad.append(f"{os.path.relpath(p, ROOT)}:{ln}: {m.group(0)} "
                                    f"(file has {max(counts)} lines)")
     assert not bad, "\n".join(bad)
+
+
+OWN = re.compile(r"\b((?:tests|tools|oracle|profiles|include|cs3602-llm-inference-acceleration_amd)"
+                 r"/[\w./-]*\w\.(?:py|cpp|hip|h|c|sh|json|jsonl|csv|txt|md|npz))\b")
+
+
+def test_repo_file_citations_exist():
+    """Every path of this repo's own files named in its sources and docs (csrc comments
+    included) exists -- a stale file reference is as misleading as a stale line number."""
+    bad = []
+    for root, dirs, fs in os.walk(ROOT):
+        dirs[:] = [d for d in dirs if d not in (".git", "gpurun_out", "profiles", "__pycache__",
+                                                "_build", "_lib")]
+        for f in fs:
+            if not f.endswith((".py", ".h", ".hip", ".cpp", ".c", ".sh", ".md")) or f in SKIP_DOCS:
+                continue
+            p = os.path.join(root, f)
+            for ln, line in enumerate(open(p, errors="ignore"), 1):
+                for m in OWN.finditer(line):
+                    path = m.group(1)
+                    if "*" in path or "<" in path:
+                        continue
+                    if not os.path.exists(os.path.join(ROOT, path)):
+                        bad.append(f"{os.path.relpath(p, ROOT)}:{ln}: {path}")
+    assert not bad, "\n".join(bad)

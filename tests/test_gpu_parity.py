@@ -419,3 +419,33 @@ def test_misaligned_contiguous_views_take_the_general_path():
     out = fix_size_l2_compress([(k, v)], fix_kv_size=100, skip_layers=[])
     rk, rv, _ = oracle.fix_size_l2_compress([(kn, vn)], fix_kv_size=100, skip_layers=[])[0]
     assert np.array_equal(to_np(out[0][0]), rk) and np.array_equal(to_np(out[0][1]), rv)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16", "fp32"])
+@pytest.mark.parametrize("variant", ["normal", "few", "equal", "special"])
+def test_mid_length_zones_four_rows_per_cu(dtype, variant, launch_path):
+    """Zones of 4 097..8 192 positions run the 512-thread rows whose LDS is budgeted for four
+    rows per CU: 16-bit keys with rank windows (levels of 'equal' / 'few' rows swap more pairs
+    than a window holds), fp32 keys with full tables.  Sort (fix_size_l2 keep_low / keep_high),
+    topk (snapkv_lite) and segment layouts (h2o_l2) against the oracle."""
+    from kvcompress.methods import fix_size_l2_compress, h2o_l2_compress, snapkv_lite_compress
+    for S in (4097, 6000, 8192):
+        layers_np = [(prng.gen_keys(8100 + S + i, (1, 2, S, 64), dtype, variant),
+                      prng.gen_values(8100 + S + i, (1, 2, S, 64), dtype)) for i in range(2)]
+        tin = [(to_dev(k), to_dev(v)) for k, v in layers_np]
+        for fn, ofn, kw in (
+                (fix_size_l2_compress, oracle.fix_size_l2_compress,
+                 dict(fix_kv_size=512, skip_layers=[])),
+                (fix_size_l2_compress, oracle.fix_size_l2_compress,
+                 dict(fix_kv_size=S // 2, keep_ratio=0.25, strategy="keep_high", skip_layers=[])),
+                (snapkv_lite_compress, oracle.snapkv_lite_compress,
+                 dict(observation_window=32, keep_size=2000)),
+                (h2o_l2_compress, oracle.h2o_l2_compress,
+                 dict(start_size=4, heavy_hitter_size=S // 3, recent_size=300))):
+            out = fn(list(tin), **kw)
+            ref = ofn(layers_np, **kw)
+            bits = {2: np.uint16, 4: np.uint32}
+            for (ko, vo), (rk, rv, _) in zip(out, ref):  # bit patterns: NaN keys are kept rows
+                b = bits[rk.dtype.itemsize]
+                assert np.array_equal(to_np(ko).view(b), rk.view(b)) and \
+                    np.array_equal(to_np(vo).view(b), rv.view(b)), (S, fn.__name__, kw)
