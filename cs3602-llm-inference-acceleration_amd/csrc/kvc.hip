@@ -50,6 +50,10 @@ constexpr int kZoneMax = 16384;        // longest zone whose selection runs from
 constexpr int kZoneMaxGlobal = 65536;  // longest zone of the u16-position global variant
 constexpr int kZoneMaxLong = 1 << 24;   // longest zone at all (u32 positions; global scratch)
 constexpr int kWaveSeg = 256;  // segments this short are finished by one wave (64 / 128 / 512 / 1024 measured slower)
+#ifndef KVC_WAVE_SEG_SMALL
+#define KVC_WAVE_SEG_SMALL 256
+#endif
+constexpr int kWaveSegSmall = KVC_WAVE_SEG_SMALL;  // the same for 512-thread rows
 constexpr int kGatherThreads = 256;
 constexpr int kGatherTokens = 64;  // output tokens per gather block
 constexpr int kBig = 0x7FFFFFFF;
@@ -514,11 +518,17 @@ __device__ __forceinline__ void snapkv_keys16(const char* nrow, int n, int pool_
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
       uint32_t pk = 0;
+      if constexpr (DT == KVC_BF16) {  // one hardware convert per pair (NaN payloads unobserved)
+        pk = f32x2_to_bf16x2_hw(m - bf16_to_f32(w[h]), m - bits_to_f32(w[h] & 0xFFFF0000u));
+        const int i0 = v * 8 + 2 * h;
+        pk &= (i0 + 1 < n ? 0xFFFFFFFFu : i0 < n ? 0x0000FFFFu : 0u);
+      } else {
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const uint32_t u = (w[h] >> (16 * b)) & 0xFFFFu;
-        const float f = in16<DT>(u);
-        pk |= (v * 8 + 2 * h + b < n ? out16<DT>(m - f) : 0u) << (16 * b);
+        for (int b = 0; b < 2; ++b) {
+          const uint32_t u = (w[h] >> (16 * b)) & 0xFFFFu;
+          const float f = in16<DT>(u);
+          pk |= (v * 8 + 2 * h + b < n ? out16<DT>(m - f) : 0u) << (16 * b);
+        }
       }
       o[h] = pk;
     }
@@ -560,27 +570,69 @@ __device__ __forceinline__ void snapkv_keys16(const char* nrow, int n, int pool_
       }
     }
     uint32_t o[4] = {0, 0, 0, 0};
+    if constexpr (DT == KVC_BF16) {
+      // bf16: pairs of positions with packed fp32 adds, one hardware convert and one packed key
+      // map per pair (key_bf16x2 codes for every key of the row).  The window sums drop
+      // avg_pool1d's leading 0 + s: it only turns a -0 into +0, and the keys equate the two.
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      const bool inner = pool && v >= 1 && v * 8 + 10 <= n;  // every window of the vector whole
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int i = v * 8 + e;
-      float r;
-      if (pool) {  // pool_k == 5, pad 2: window [i - 2, i + 3) clipped to [0, n), / 5
-        int hs = i - 2;
-        int he = min(hs + 5, n + 2);
-        const int psize = he - hs;
-        hs = max(hs, 0);
-        he = min(he, n);
-        float sum = 0.f;
+      for (int p = 0; p < 4; ++p) {
+        f2 r;
+        if (inner) {
+          f2 acc = f2{sw[2 * p + 6], sw[2 * p + 7]};
 #pragma unroll
-        for (int t = 0; t < 5; ++t) {
-          const int j = i - 2 + t;
-          if (j >= hs && j < he) sum = sum + sw[8 + e - 2 + t];
+          for (int t = 1; t < 5; ++t) acc = acc + f2{sw[2 * p + 6 + t], sw[2 * p + 7 + t]};
+          r = f2{div5_rn(acc.x), div5_rn(acc.y)};
+        } else {
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            const int e = 2 * p + b, i = v * 8 + e;
+            float x = sw[8 + e];
+            if (pool) {  // pool_k == 5, pad 2: window [i - 2, i + 3) clipped to [0, n), / 5
+              int hs = i - 2;
+              int he = min(hs + 5, n + 2);
+              const int psize = he - hs;
+              hs = max(hs, 0);
+              he = min(he, n);
+              float sum = 0.f;
+#pragma unroll
+              for (int t = 0; t < 5; ++t) {
+                const int j = i - 2 + t;
+                if (j >= hs && j < he) sum = sum + sw[8 + e - 2 + t];
+              }
+              x = psize == 5 ? div5_rn(sum) : sum / (float)psize;
+            }
+            r[b] = x;
+          }
         }
-        r = psize == 5 ? div5_rn(sum) : sum / (float)psize;
-      } else {
-        r = sw[8 + e];
+        const int i0 = v * 8 + 2 * p;
+        o[p] = key_bf16x2(f32x2_to_bf16x2_hw(r.x, r.y), desc) &
+               (i0 + 1 < n ? 0xFFFFFFFFu : i0 < n ? 0x0000FFFFu : 0u);
       }
-      o[e >> 1] |= (i < n ? (uint32_t)key16_dt<DT>(out16<DT>(r), desc) : 0u) << (16 * (e & 1));
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int i = v * 8 + e;
+        float r;
+        if (pool) {  // pool_k == 5, pad 2: window [i - 2, i + 3) clipped to [0, n), / 5
+          int hs = i - 2;
+          int he = min(hs + 5, n + 2);
+          const int psize = he - hs;
+          hs = max(hs, 0);
+          he = min(he, n);
+          float sum = 0.f;
+#pragma unroll
+          for (int t = 0; t < 5; ++t) {
+            const int j = i - 2 + t;
+            if (j >= hs && j < he) sum = sum + sw[8 + e - 2 + t];
+          }
+          r = psize == 5 ? div5_rn(sum) : sum / (float)psize;
+        } else {
+          r = sw[8 + e];
+        }
+        o[e >> 1] |= (i < n ? (uint32_t)key16_dt<DT>(out16<DT>(r), desc) : 0u) << (16 * (e & 1));
+      }
     }
     reinterpret_cast<uint4*>(key)[v] = make_uint4(o[0], o[1], o[2], o[3]);
   }
@@ -2205,7 +2257,7 @@ static int launch_select(const LayerChunk& T, int cn, int BH, int dt, int order,
     const int cap = sel_cap(n_cap, ks, kSmallBudget);
     return launch_k(select_kernel<KC, kSelThreadsSmall>, rows_grid, dim3(kSelThreadsSmall),
                     sel_bytes(n_cap, ks, cap), s, T, BH, dt, order, algo, norms, nstride, idx,
-                    istride, kWaveSeg, n_cap, cap, stamps, status);
+                    istride, kWaveSegSmall, n_cap, cap, stamps, status);
   }
   return launch_k(select_kernel<KC, kSelThreads>, rows_grid, dim3(kSelThreads), 0, s, T, BH, dt,
                   order, algo, norms, nstride, idx, istride, kWaveSeg, n_cap, 0, stamps, status);
@@ -2256,7 +2308,7 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
         const int cap = sel_cap(n_cap, ks, kSmallBudget);
         return launch_k(select_gather_kernel<KC, kSelThreadsSmall, NC>, rows_grid,
                         dim3(kSelThreadsSmall), sel_bytes(n_cap, ks, cap), s, T, H, BH, DT,
-                        p->order, p->algo, norms, nstride, kWaveSeg, n_cap, cap, status);
+                        p->order, p->algo, norms, nstride, kWaveSegSmall, n_cap, cap, status);
       }
       return launch_k(select_gather_kernel<KC, kSelThreads, NC>, rows_grid, dim3(kSelThreads), 0,
                       s, T, H, BH, DT, p->order, p->algo, norms, nstride, kWaveSeg, n_cap, 0,

@@ -80,6 +80,32 @@ __device__ __forceinline__ uint32_t f32_to_f16_hw(float f) {
   return __builtin_bit_cast(uint16_t, (_Float16)f);
 }
 
+// fp32 pair -> packed bf16 pair with the hardware convert (v_cvt_pk_bf16_f32: IEEE round to
+// nearest even, fp32 denormals kept -- the gfx950 default mode).  Bit-identical to
+// f32_to_bf16_rne on every non-NaN input and NaN for every NaN input (payload / sign may differ),
+// so it serves where a NaN is only tested or mapped to a key (the snapkv scores);
+// tests/native/cvt16_check.hip checks all 2^32 inputs on the GPU.
+__device__ __forceinline__ uint32_t f32x2_to_bf16x2_hw(float lo, float hi) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2{lo, hi}, b2));
+}
+
+// Sort keys of two packed bf16 values with packed 16-bit integer ops: k = 0x8000 + mag for
+// positive, 0x8000 - mag for negative values (+-0 -> 0x8000), every NaN -> 0xFFFF; desc = ~k.
+// Same order and the same ties as key_bf16 (PyTorch's comparators), not the same codes: use it
+// for every key of a row or for none.
+__device__ __forceinline__ uint32_t key_bf16x2(uint32_t w, bool desc) {
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  const u16x2 b = __builtin_bit_cast(u16x2, w);
+  const u16x2 mag = b & (u16x2)0x7FFF;
+  const u16x2 neg = (u16x2)0 - (b >> 15);                      // 0xFFFF where negative
+  const u16x2 nan = (u16x2)0 - ((mag + (u16x2)0x7F) >> 15);    // 0xFFFF where mag > 0x7F80
+  u16x2 k = ((u16x2)0x8000 + ((mag ^ neg) - neg)) | nan;       // 0x8000 +- mag (mod 2^16)
+  if (desc) k = ~k;
+  return __builtin_bit_cast(uint32_t, k);
+}
+
 // Sort keys.  Ascending base order is PyTorch's asc comparator
 //   (!isnan(a) && isnan(b)) || a < b
 // i.e. numeric order with -0 == +0 and every NaN tied above +inf.  Descending order
