@@ -50,10 +50,9 @@ constexpr int kZoneMax = 16384;        // longest zone whose selection runs from
 constexpr int kZoneMaxGlobal = 65536;  // longest zone of the u16-position global variant
 constexpr int kZoneMaxLong = 1 << 24;   // longest zone at all (u32 positions; global scratch)
 constexpr int kWaveSeg = 256;  // segments this short are finished by one wave (64 / 128 / 512 / 1024 measured slower)
-#ifndef KVC_WAVE_SEG_SMALL
-#define KVC_WAVE_SEG_SMALL 256
-#endif
-constexpr int kWaveSegSmall = KVC_WAVE_SEG_SMALL;  // the same for 512-thread rows
+// the same for 512-thread rows (128 / 512 / 1 024 measured the same or slower at S = 4 096 and
+// 8 192: profiles/r03_g_small_wave_threshold_ab.jsonl)
+constexpr int kWaveSegSmall = 256;
 constexpr int kGatherThreads = 256;
 constexpr int kGatherTokens = 64;  // output tokens per gather block
 constexpr int kBig = 0x7FFFFFFF;
@@ -669,6 +668,35 @@ __device__ __forceinline__ void wave_stable_sort(KeyT* key, uint16_t* idx, int l
     key[lo + r] = (KeyT)kk;
     idx[lo + r] = ii;
   }
+}
+
+// std::__heap_select(first, first + middle, first + len) -- std::partial_sort's selection, which
+// torch.topk uses when k * 64 <= n (aten TopKImpl.h) -- run by one wave: lane 0 builds the heap
+// and performs every pop_heap exactly as libstdc++ does (kvc_serial.h), while the wave scans the
+// candidates 64 at a time: element i enters iff key[i] < key[0] at its turn, and key[0] only
+// decreases, so a ballot against the current top leaves exactly the elements the serial loop
+// would pop, in index order (re-checked against the new top after each pop).  The scan of the
+// n - middle elements no longer costs one dependent LDS round trip each.  Call with all 64
+// lanes of one wave; positions >= middle other than the popped one are never written.
+template <typename K, typename I>
+__device__ __forceinline__ void wave_heap_select(K* key, I* idx, int middle, int len) {
+  const int lane = threadIdx.x & 63;
+  if (lane == 0) make_heap(key, idx, middle);
+  wave_sync();
+  uint32_t top = (uint32_t)key[0];
+  for (int base = middle; base < len; base += 64) {
+    const int i = base + lane;
+    const uint32_t ki = i < len ? (uint32_t)key[i] : 0xFFFFFFFFu;
+    uint64_t cand = __builtin_amdgcn_ballot_w64(i < len && ki < top);
+    while (cand) {
+      const int l = (int)__builtin_ctzll(cand);
+      if (lane == 0) pop_heap(key, idx, middle, base + l);
+      wave_sync();
+      top = (uint32_t)key[0];
+      cand &= ~((2ull << l) - 1ull) & __builtin_amdgcn_ballot_w64(ki < top);
+    }
+  }
+  wave_sync();
 }
 
 // The partition chain of libstdc++ introsort (topk = false) / introselect (topk = true),
@@ -1383,7 +1411,7 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
   const bool partial = topk && (int64_t)k * 64 <= n;  // aten TopKImpl.h: use_partial_sort
   const int thr = topk ? 3 : 16;  // introselect / introsort segment threshold
   if (partial) {
-    if (tid == 0) heap_select(key, idx, k, n);  // std::partial_sort's heap select
+    if (wid == 0) wave_heap_select(key, idx, k, n);  // std::partial_sort's heap select
   } else {
     int lo = 0, hi = n, depth = 2 * floor_log2(n), level = 0;
     uint64_t* accb = nullptr;
@@ -1658,8 +1686,8 @@ __global__ void __launch_bounds__(kSelThreads)
   for (int i = tid; i < n; i += kSelThreads) idx[i] = (uint32_t)i;
   __syncthreads();
   const bool topk = algo == KVC_ALGO_TOPK;
-  if (topk && (int64_t)k * 64 <= n) {  // std::partial_sort's heap select (one lane)
-    if (tid == 0) heap_select(key, idx, k, n);
+  if (topk && (int64_t)k * 64 <= n) {  // std::partial_sort's heap select (one wave)
+    if (wid == 0) wave_heap_select(key, idx, k, n);
   } else {
     const int thr = topk ? 3 : 16;
     int lo = 0, hi = n, depth = 2 * floor_log2(n);

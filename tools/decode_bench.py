@@ -66,6 +66,24 @@ for name, kw, S in cases:
     kv = layers_of(S)
     fn = get_compress_fn(name)
     res[name] = {"S": S, "engine_ms_per_step": round(timeit(lambda: fn(list(kv), **kw)), 4)}
+# h2o_attention: per step the manager accumulates one query row of attention per layer, then the
+# heavy hitters (head sum + topk) and the compaction -- S = 513, heavy_hitter_size 64 / recent 444
+from kvcompress.methods.h2o_attention import H2OAttentionManager, h2o_attention_compress  # noqa
+kv = layers_of(513)
+att = tuple(torch.softmax(torch.randn(1, H, 1, 513, device=dev, generator=g), -1).to(torch.bfloat16)
+            for _ in range(L))
+mgr = H2OAttentionManager(start_size=4, heavy_hitter_size=64, recent_size=444)
+res["h2o_attention"] = {"S": 513, "engine_ms_per_step": round(timeit(
+    lambda: h2o_attention_compress(list(kv), attention_scores=att, h2o_manager=mgr,
+                                   skip_layers=[])), 4)}
+# a long-context call: heavy hitters over a 15 936-position middle (std::partial_sort path)
+kv = layers_of(16384)
+att = tuple(torch.softmax(torch.randn(1, H, 1, 16384, device=dev, generator=g), -1).to(torch.bfloat16)
+            for _ in range(L))
+mgr = H2OAttentionManager(start_size=4, heavy_hitter_size=64, recent_size=444)
+res["h2o_attention_s16384"] = {"S": 16384, "engine_ms_per_call": round(timeit(
+    lambda: h2o_attention_compress(list(kv), attention_scores=att, h2o_manager=mgr,
+                                   skip_layers=[]), reps=10), 4)}
 kv = layers_of(513)
 res["fix_size_l2"]["reference_ops_on_gpu_ms_per_step"] = round(
     timeit(lambda: ref_fix_size_torch(kv, 512)), 4)
