@@ -28,6 +28,12 @@ layers = [(torch.randn(1, 32, S, 128, device=dev, generator=g).to(dt),
           for _ in range(32)]
 fn = get_compress_fn(method)
 call = lambda: fn(layers, skip_layers=[], **kw)  # noqa: E731
+if method == "h2o_attention":  # one query row of attention per layer and step, a manager
+    from kvcompress.methods.h2o_attention import H2OAttentionManager
+    att = tuple(torch.softmax(torch.randn(1, 32, 1, S, device=dev, generator=g), -1).to(dt)
+                for _ in range(32))
+    mgr = H2OAttentionManager(**kw)
+    call = lambda: fn(layers, attention_scores=att, h2o_manager=mgr, skip_layers=[], **kw)  # noqa
 for _ in range(20):
     call()
 torch.cuda.synchronize()
