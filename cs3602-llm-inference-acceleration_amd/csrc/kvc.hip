@@ -30,8 +30,6 @@
 namespace kvc {
 
 constexpr int kTile = 64;  // tokens per score tile (one per lane)
-constexpr int kScoreThreads = 256;
-constexpr int kScoreWaves = kScoreThreads / 64;
 constexpr int kSelThreads = 1024;
 constexpr int kSelWaves = kSelThreads / 64;
 // Zones of up to kSmallZone positions select with 512-thread workgroups and LDS sized by the
@@ -216,6 +214,14 @@ __device__ __forceinline__ void accum_chunk(float (&acc)[8], const uint4 x, int 
 // 16-B chunks of a token row staged per phase: 4 (64-B rows), 8 (multiples of 128 B), 10 (160 B
 // multiples); a row of NC chunks takes NC / CP phases.
 __host__ __device__ constexpr int score_cp(int nc) { return nc == 4 ? 4 : (nc % 8 == 0 ? 8 : 10); }
+// padded LDS row of CP chunks: an odd number of 16-B granules keeps every lane's ds_read_b128 of
+// its own token row conflict-free
+__host__ __device__ constexpr int score_rowb(int cp) { return (cp + (cp % 2 == 0 ? 1 : 2)) * 16; }
+// waves (tiles) per workgroup: 8 for CP-8 rows (9.2 KB slab per wave: two 74 KB workgroups per
+// CU, 2.5% faster than four 4-wave ones), 4 otherwise (the 10-chunk slab is 12.3 KB per wave:
+// three 4-wave workgroups fit a CU, one 8-wave one -- measured 45% slower at D=80).  A/B in
+// profiles/r03_j_score_variants_ab.jsonl.
+__host__ __device__ constexpr int score_waves(int nc) { return score_cp(nc) == 8 ? 8 : 4; }
 
 // One 64-token tile of one (layer, b, h) row: coalesced 16-B loads -> per-wave LDS slab ->
 // one lane per token, torch.norm's 8-accumulator FMA order (fp16: its serial order).  `wl` is
@@ -226,7 +232,7 @@ __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int t
   constexpr int ESZ = DTypeTraits<DT>::esz;
   constexpr int CP = score_cp(NC);  // 16-B chunks per token per phase
   constexpr int NPH = NC / CP;
-  constexpr int ROWB = CP * 16 + 16;  // padded LDS row: conflict-free ds_read_b128 per lane
+  constexpr int ROWB = score_rowb(CP);  // padded LDS row: conflict-free ds_read_b128 per lane
   const int lane = threadIdx.x & 63;
   const int zlen = ly->zone_len;
   const int b = row / H, h = row - (row / H) * H;
@@ -277,21 +283,24 @@ __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int t
     for (int j = 1; j < 8; ++j) s = s + acc[j];
     const float r = __builtin_sqrtf(s);
     char* nrow = norms + (int64_t)(ly->row0 + row) * norm_stride * ESZ;
+    // non-temporal: the select phase reads the norms back from the Infinity Cache, not from
+    // this XCD's L2, so keeping them in L2 only evicts key lines (2.5% faster score pass)
     if constexpr (DT != KVC_F32) {
-      uint16_t* d = reinterpret_cast<uint16_t*>(nrow) + tok0 + lane;
-      *d = (uint16_t)bits16_dt<DT>(r);
+      __builtin_nontemporal_store((uint16_t)bits16_dt<DT>(r),
+                                  reinterpret_cast<uint16_t*>(nrow) + tok0 + lane);
     } else {
-      reinterpret_cast<float*>(nrow)[tok0 + lane] = r;
+      __builtin_nontemporal_store(r, reinterpret_cast<float*>(nrow) + tok0 + lane);
     }
   }
 }
 
 template <int DT, int NC, bool NTL>
-__global__ void __launch_bounds__(kScoreThreads)
+__global__ void __launch_bounds__(score_waves(NC) * 64)
     score_kernel(const LayerChunk T, int nl, int H, int64_t tile_base, int64_t chunk_tiles,
                  char* __restrict__ norms, int64_t norm_stride) {
   constexpr int CP = score_cp(NC);
-  constexpr int ROWB = CP * 16 + 16;
+  constexpr int ROWB = score_rowb(CP);
+  constexpr int kScoreWaves = score_waves(NC);
   __shared__ __attribute__((aligned(16))) char lds[kScoreWaves][kTile * ROWB];
   const kvc_layer_t* L = T.l;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2245,8 +2254,9 @@ static int with_nc(int nc, F&& f) {
 template <int DT, int NC>
 static int launch_score(const LayerChunk& T, int nl, int H, int64_t tile_base,
                         int64_t chunk_tiles, char* norms, int64_t nstride, hipStream_t s) {
-  const unsigned grid = (unsigned)((chunk_tiles + kScoreWaves - 1) / kScoreWaves);
-  return launch_k(score_kernel<DT, NC, true>, dim3(grid), dim3(kScoreThreads), 0, s, T, nl, H,
+  constexpr int per_wg = score_waves(NC);  // one tile per wave
+  const unsigned grid = (unsigned)((chunk_tiles + per_wg - 1) / per_wg);
+  return launch_k(score_kernel<DT, NC, true>, dim3(grid), dim3(per_wg * 64), 0, s, T, nl, H,
                   tile_base, chunk_tiles, norms, nstride);
 }
 

@@ -38,7 +38,7 @@ fp32 add, rounded to the dtype.
 
 Pinned by tests/test_h2o_oracle.py against torch's own CPU ops (sums across shapes and thread
 counts, AVX512 and AVX2 capabilities) and against the unmodified reference's outputs in
-tests/golden/h2o_attention_ties.npz (tests/golden/gen_h2o_attention_ties.py).
+tests/golden/h2o_attention_ties.json (tests/golden/gen_h2o_attention_ties.py).
 """
 import numpy as np
 

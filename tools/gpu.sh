@@ -59,7 +59,7 @@ for step in "$@"; do
       tail -c 3000 "$O/pmc_round.out" ;;
     ab)
       : > "$O/ab.jsonl"
-      for rep in 1 2; do
+      for rep in ${AB_REPS:-1 2}; do
         for lib in ${AB_LIBS:?}; do
           for w in ${AB_WORKLOADS:-fix512-s16384}; do
             KVC_LIB="$LIBDIR/$lib" timeout -k 10 200 python bench.py --workload $w --steps 20 \
