@@ -143,15 +143,28 @@ __device__ __forceinline__ void with_dt(int dt, F&& f) {
 }
 __device__ __forceinline__ uint32_t inf_bits16(int dt) { return dt == KVC_F16 ? 0x7C00u : 0x7F80u; }
 
-// torch.gather's NaN rewrite on two 16-bit elements (bf16: 0xFFFF; fp16: quiet bit); fp32 none
+// torch.gather's NaN rewrite on two 16-bit elements (kvc_common.h canon_nan_bf16x2 /
+// canon_nan_f16x2) in five packed-u16 VALU ops instead of two compare/select chains:
+// x = |w| per half; x + (0xFFFE - NANMIN) saturates to 0xFFFF exactly for x > NANMIN (a NaN);
+// that - 0xFFFE (saturating) is 1 for a NaN half and 0 otherwise, scaled to the bits to set.
+// Equal to the scalar forms on all 2^32 inputs (checked exhaustively when it was written).
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+template <uint16_t NANMIN, uint16_t SET>
+__device__ __forceinline__ uint32_t canon_nan_pk(uint32_t w) {
+  const u16x2 x = __builtin_bit_cast(u16x2, w & 0x7FFF7FFFu);
+  const u16x2 m = __builtin_elementwise_add_sat(
+      x, (u16x2){(uint16_t)(0xFFFEu - NANMIN), (uint16_t)(0xFFFEu - NANMIN)});
+  const u16x2 t = __builtin_elementwise_sub_sat(m, (u16x2){0xFFFE, 0xFFFE});
+  return w | __builtin_bit_cast(uint32_t, t * (u16x2){SET, SET});
+}
 template <int DT>
 __device__ __forceinline__ uint4 canon_nan_dt(uint4 a) {
-  if constexpr (DT == KVC_BF16)
-    return make_uint4(canon_nan_bf16x2(a.x), canon_nan_bf16x2(a.y), canon_nan_bf16x2(a.z),
-                      canon_nan_bf16x2(a.w));
-  else if constexpr (DT == KVC_F16)
-    return make_uint4(canon_nan_f16x2(a.x), canon_nan_f16x2(a.y), canon_nan_f16x2(a.z),
-                      canon_nan_f16x2(a.w));
+  if constexpr (DT == KVC_BF16)  // NaN -> 0xFFFF
+    return make_uint4(canon_nan_pk<0x7F80, 0xFFFF>(a.x), canon_nan_pk<0x7F80, 0xFFFF>(a.y),
+                      canon_nan_pk<0x7F80, 0xFFFF>(a.z), canon_nan_pk<0x7F80, 0xFFFF>(a.w));
+  else if constexpr (DT == KVC_F16)  // NaN |= 0x200 (quiet bit)
+    return make_uint4(canon_nan_pk<0x7C00, 0x200>(a.x), canon_nan_pk<0x7C00, 0x200>(a.y),
+                      canon_nan_pk<0x7C00, 0x200>(a.z), canon_nan_pk<0x7C00, 0x200>(a.w));
   else
     return a;
 }
@@ -218,10 +231,13 @@ __host__ __device__ constexpr int score_cp(int nc) { return nc == 4 ? 4 : (nc % 
 // its own token row conflict-free
 __host__ __device__ constexpr int score_rowb(int cp) { return (cp + (cp % 2 == 0 ? 1 : 2)) * 16; }
 // waves (tiles) per workgroup: 8 for CP-8 rows (9.2 KB slab per wave: two 74 KB workgroups per
-// CU, 2.5% faster than four 4-wave ones), 4 otherwise (the 10-chunk slab is 12.3 KB per wave:
-// three 4-wave workgroups fit a CU, one 8-wave one -- measured 45% slower at D=80).  A/B in
-// profiles/r03_j_score_variants_ab.jsonl.
-__host__ __device__ constexpr int score_waves(int nc) { return score_cp(nc) == 8 ? 8 : 4; }
+// CU, 2.5% faster than four 4-wave ones); 2 for CP-10 rows (11.3 KB per wave: seven 2-wave
+// workgroups per CU, 14 waves -- D = 80 score 0.1049 -> 0.1011 ms against three 4-wave ones
+// (12 waves); two 7-wave ones, also 14 waves, 0.1063; 8-wave ones 45% slower); 4 for 64-B
+// rows.  A/B in profiles/r03_j_score_variants_ab.jsonl and r03_l_select_variants.json.
+__host__ __device__ constexpr int score_waves(int nc) {
+  return score_cp(nc) == 8 ? 8 : score_cp(nc) == 10 ? 2 : 4;
+}
 
 // One 64-token tile of one (layer, b, h) row: coalesced 16-B loads -> per-wave LDS slab ->
 // one lane per token, torch.norm's 8-accumulator FMA order (fp16: its serial order).  `wl` is
@@ -800,20 +816,30 @@ __device__ __forceinline__ void p1_counts(const KeyT* key, int pos0, int J, int 
 }
 
 // P2 of a level, rank window 0: scatter the s and g rank -> position tables for ranks <= cap
-// (every ge position: g_{m+1} is then read from the table) and count the swaps (nsw), from
-// re-read keys.
-// FAST: a whole stripe without the median slot.  Otherwise lanes past hi are masked and the
-// median slot ch carries klo's flags (kge / kle): the owner wave moves the median physically
-// only after this pass.
-template <typename KeyT, int JM, bool FAST>
+// and count the swaps (nsw), from re-read keys.  With F(x) = A(x) + Lin(x) (non-decreasing in
+// x), a ge position is swapped iff F < tot_le and an le position iff F > tot_le, and only the
+// swapped g's and s's plus g_{m+1} are ever read back.  So a whole stripe (MODE):
+//   P2_FULL  straddles F = tot_le: records every ge and le rank <= cap, counts its swaps;
+//   P2_LEFT  ends at F <= tot_le: every ge swapped (nsw = its ge count, set by the caller), no
+//            le swapped -- records the g ranks only;
+//   P2_RIGHT starts at F >= tot_le: no ge swapped, every le swapped -- records the s ranks and
+//            its first ge position (g_{m+1} when no earlier stripe has an unswapped ge).
+// FAST: a whole stripe without the median slot.  Otherwise (always P2_FULL) lanes past hi are
+// masked and the median slot ch carries klo's flags (kge / kle): the owner wave moves the
+// median physically only after this pass.
+enum { P2_FULL = 0, P2_LEFT = 1, P2_RIGHT = 2 };
+template <typename KeyT, int JM, bool FAST, int MODE = P2_FULL>
 __device__ __forceinline__ void p2_window0(const KeyT* key, uint16_t* spos, uint16_t* gpos,
                                            int lane, int pos0, int wbeg, int J, int hi,
                                            uint32_t p, int ch, bool kge, bool kle, int rge1,
                                            int rle, int tot_le, int cap, int& nsw) {
+  static_assert(FAST || MODE == P2_FULL, "partial stripes take the full pass");
   // keys in flight per lane (register budget: 64 VGPRs); 4 and 16 measured the same
-  // (profiles/r03_c_p2_keys_in_flight_ab.jsonl): the level is latency-, not issue-bound
+  // (profiles/r03_c_p2_keys_in_flight_ab.jsonl)
   constexpr int JB = JM < 8 ? JM : 8;
   const int t1 = tot_le + 1;
+  const int g1 = rge1;  // P2_RIGHT: rank of the stripe's first ge position
+  int ff = kBig;        // P2_RIGHT: the stripe's first ge position (wave-uniform)
   unroll_for<0, JM / JB>([&](auto bc) {
     constexpr int j0 = decltype(bc)::value * JB;
     if (j0 > 0 && j0 >= J) return;
@@ -834,17 +860,36 @@ __device__ __forceinline__ void p2_window0(const KeyT* key, uint16_t* spos, uint
         ge = inb && (isch ? kge : ge);
         le = inb && (isch ? kle : le);
       }
-      const uint64_t bg = __builtin_amdgcn_ballot_w64(ge), bl = __builtin_amdgcn_ballot_w64(le);
-      const int a1 = mbcnt(bg, rge1);                   // g rank: A + 1
-      const int sr = t1 - (mbcnt(bl, rle) + (le ? 1 : 0));  // s rank: tot_le - Lin + 1
-      spos[(le && sr <= cap) ? sr : lane - 64] = (uint16_t)pj;
-      gpos[(ge && a1 <= cap) ? a1 : lane - 64] = (uint16_t)pj;
-      // g_t < s_t  <=>  A + Lin < tot_le  <=>  a1 < sr: swapped (a prefix t <= m of the g's)
-      nsw += __popcll(bg & __builtin_amdgcn_ballot_w64(a1 < sr));
-      rge1 += __popcll(bg);
-      rle += __popcll(bl);
+      if constexpr (MODE == P2_LEFT) {
+        const uint64_t bg = __builtin_amdgcn_ballot_w64(ge);
+        const int a1 = mbcnt(bg, rge1);
+        gpos[(ge && a1 <= cap) ? a1 : lane - 64] = (uint16_t)pj;
+        rge1 += __popcll(bg);
+      } else if constexpr (MODE == P2_RIGHT) {
+        const uint64_t bl = __builtin_amdgcn_ballot_w64(le);
+        const int sr = t1 - (mbcnt(bl, rle) + (le ? 1 : 0));
+        spos[(le && sr <= cap) ? sr : lane - 64] = (uint16_t)pj;
+        rle += __popcll(bl);
+        if (ff == kBig) {
+          const uint64_t bg = __builtin_amdgcn_ballot_w64(ge);
+          if (bg) ff = pj - lane + (int)__builtin_ctzll(bg);
+        }
+      } else {
+        const uint64_t bg = __builtin_amdgcn_ballot_w64(ge), bl = __builtin_amdgcn_ballot_w64(le);
+        const int a1 = mbcnt(bg, rge1);                   // g rank: A + 1
+        const int sr = t1 - (mbcnt(bl, rle) + (le ? 1 : 0));  // s rank: tot_le - Lin + 1
+        spos[(le && sr <= cap) ? sr : lane - 64] = (uint16_t)pj;
+        gpos[(ge && a1 <= cap) ? a1 : lane - 64] = (uint16_t)pj;
+        // g_t < s_t  <=>  A + Lin < tot_le  <=>  a1 < sr: swapped (a prefix t <= m of the g's)
+        nsw += __popcll(bg & __builtin_amdgcn_ballot_w64(a1 < sr));
+        rge1 += __popcll(bg);
+        rle += __popcll(bl);
+      }
     });
   });
+  if constexpr (MODE == P2_RIGHT) {
+    if (ff != kBig && g1 <= cap && lane == 0) gpos[g1] = (uint16_t)ff;
+  }
 }
 
 // One partition level over [lo, hi) with at most JM positions per lane (compile-time bound; the
@@ -925,10 +970,19 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
   KVC_TICK(t1);
   // ---- P2, rank window 0: s / g rank tables, swap count m, g_{m+1} (stores only) ----
   int nsw = 0;
-  if (whole && !owner)
-    p2_window0<KeyT, JM, true>(key, spos, gpos, lane, pos0, wbeg, J, hi, p, ch, kge, kle,
-                               ge_before + 1, le_before, tot_le, cap, nsw);
-  else if (nval > 0)
+  if (whole && !owner) {
+    if (ge_before + cge + le_before + cle <= tot_le) {  // every ge swapped, no le
+      p2_window0<KeyT, JM, true, P2_LEFT>(key, spos, gpos, lane, pos0, wbeg, J, hi, p, ch, kge,
+                                          kle, ge_before + 1, le_before, tot_le, cap, nsw);
+      nsw = cge;
+    } else if (ge_before + le_before >= tot_le) {  // no ge swapped, every le
+      p2_window0<KeyT, JM, true, P2_RIGHT>(key, spos, gpos, lane, pos0, wbeg, J, hi, p, ch, kge,
+                                           kle, ge_before + 1, le_before, tot_le, cap, nsw);
+    } else {
+      p2_window0<KeyT, JM, true>(key, spos, gpos, lane, pos0, wbeg, J, hi, p, ch, kge, kle,
+                                 ge_before + 1, le_before, tot_le, cap, nsw);
+    }
+  } else if (nval > 0)
     p2_window0<KeyT, JM, false>(key, spos, gpos, lane, pos0, wbeg, J, hi, p, ch, kge, kle,
                                 ge_before + 1, le_before, tot_le, cap, nsw);
   // the median move, made physical by the only wave that reads slot ch (after its P2 loads)
@@ -1337,6 +1391,9 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
     return true;
   }
   const bool desc = order == KVC_DESC;
+  const bool topk = algo == KVC_ALGO_TOPK;
+  const bool partial = topk && (int64_t)k * 64 <= n;  // aten TopKImpl.h: use_partial_sort
+  const int thr = topk ? 3 : 16;  // introselect / introsort segment threshold
 
   // ---- keys ----
   if (ly->score_mode == KVC_SCORE_SNAPKV) {
@@ -1384,11 +1441,12 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
         const uint32_t w[4] = {buf[q].x, buf[q].y, buf[q].z, buf[q].w};
         uint32_t kw[4], iw[4];
         if constexpr (KC != KVC_F32) {
+          // packed key map (key_h16x2): key_h16's order and ties, other codes -- every key of
+          // the row is made here, and the selection only compares keys with each other
           const uint32_t inf = inf_bits16(dt);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            kw[e] = (uint32_t)key_h16(w[e] & 0xFFFFu, desc, inf) |
-                    ((uint32_t)key_h16(w[e] >> 16, desc, inf) << 16);
+            kw[e] = key_h16x2(w[e], desc, inf);
             iw[e] = (uint32_t)(v * 8 + 2 * e) | ((uint32_t)(v * 8 + 2 * e + 1) << 16);
           }
           *reinterpret_cast<uint4*>(key + v * 8) = make_uint4(kw[0], kw[1], kw[2], kw[3]);
@@ -1416,9 +1474,6 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
       return true;
     }
   }
-  const bool topk = algo == KVC_ALGO_TOPK;
-  const bool partial = topk && (int64_t)k * 64 <= n;  // aten TopKImpl.h: use_partial_sort
-  const int thr = topk ? 3 : 16;  // introselect / introsort segment threshold
   if (partial) {
     if (wid == 0) wave_heap_select(key, idx, k, n);  // std::partial_sort's heap select
   } else {
@@ -1842,32 +1897,36 @@ __host__ __device__ __forceinline__ bool layer_selects(const kvc_layer_t& y) {
 
 // Copy one output row (sink ++ selected ++ tail) of K and V with the whole workgroup.
 // sel: ascending zone-local kept indices in LDS, or nullptr when no selection ran.
+// Thread tid copies 16-B chunk tid % NC of output tokens tid / NC + i * (NT / NC): the same
+// coalesced units as a flat unit loop (consecutive threads, consecutive 16-B units) with the
+// chunk and its address offsets fixed per thread; the last NT % NC threads idle.
 template <int DT, int NC, int NT = kSelThreads, bool NTS = false>
 __device__ __forceinline__ void gather_row(const kvc_layer_t* __restrict__ ly, int r, int H,
                                            const uint16_t* sel) {
   constexpr int ESZ = DTypeTraits<DT>::esz;
   constexpr int BATCH = 4;
+  constexpr int TPI = NT / NC;  // tokens per pass
+  static_assert(TPI >= 1, "a row's chunks must fit the workgroup");
+  const int tq = (int)threadIdx.x / NC, c = (int)threadIdx.x - tq * NC;
+  if (tq >= TPI) return;
   const int n_out = ly->n_out;
-  const int nu = n_out * NC;
   const int b = r / H, h = r - (r / H) * H;
   const int sink = ly->sink_len, nsel = ly->n_select;
   const char* kb = static_cast<const char*>(ly->k) +
-                   ((int64_t)b * ly->k_stride[0] + (int64_t)h * ly->k_stride[1]) * ESZ;
+                   ((int64_t)b * ly->k_stride[0] + (int64_t)h * ly->k_stride[1]) * ESZ + c * 16;
   const char* vb = static_cast<const char*>(ly->v) +
-                   ((int64_t)b * ly->v_stride[0] + (int64_t)h * ly->v_stride[1]) * ESZ;
+                   ((int64_t)b * ly->v_stride[0] + (int64_t)h * ly->v_stride[1]) * ESZ + c * 16;
   const int64_t kss = ly->k_stride[2] * ESZ, vss = ly->v_stride[2] * ESZ;
-  char* ko = static_cast<char*>(ly->k_out) + (int64_t)r * nu * 16;
-  char* vo = static_cast<char*>(ly->v_out) + (int64_t)r * nu * 16;
-  const int tid0 = (int)threadIdx.x;
-  for (int u0 = 0; u0 < nu; u0 += NT * BATCH) {
+  char* ko = static_cast<char*>(ly->k_out) + (int64_t)r * n_out * NC * 16 + c * 16;
+  char* vo = static_cast<char*>(ly->v_out) + (int64_t)r * n_out * NC * 16 + c * 16;
+  for (int tb = tq; tb < n_out; tb += TPI * BATCH) {
     uint4 xk[BATCH], xv[BATCH];
     bool gat[BATCH];
 #pragma unroll
     for (int i = 0; i < BATCH; ++i) {
-      const int u = u0 + tid0 + i * NT;
+      const int t = tb + i * TPI;
       gat[i] = false;
-      if (u < nu) {
-        const int t = u / NC, c = u - (u / NC) * NC;
+      if (t < n_out) {
         int src;
         if (t < sink) {
           src = t;
@@ -1879,28 +1938,29 @@ __device__ __forceinline__ void gather_row(const kvc_layer_t* __restrict__ ly, i
         } else {
           src = ly->tail_start + (t - sink - nsel);
         }
-        xk[i] = *reinterpret_cast<const uint4*>(kb + src * kss + c * 16);
-        xv[i] = *reinterpret_cast<const uint4*>(vb + src * vss + c * 16);
+        xk[i] = *reinterpret_cast<const uint4*>(kb + src * kss);
+        xv[i] = *reinterpret_cast<const uint4*>(vb + src * vss);
       }
     }
 #pragma unroll
     for (int i = 0; i < BATCH; ++i) {
-      const int u = u0 + tid0 + i * NT;
-      if (u < nu) {
+      const int t = tb + i * TPI;
+      if (t < n_out) {
         uint4 a = xk[i], q = xv[i];
         if (gat[i]) {
           a = canon_nan_dt<DT>(a);
           q = canon_nan_dt<DT>(q);
         }
+        const int64_t off = (int64_t)t * (NC * 16);
         if constexpr (NTS) {  // written once: non-temporal
           typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
           __builtin_nontemporal_store(u32x4{a.x, a.y, a.z, a.w},
-                                      reinterpret_cast<u32x4*>(ko + (int64_t)u * 16));
+                                      reinterpret_cast<u32x4*>(ko + off));
           __builtin_nontemporal_store(u32x4{q.x, q.y, q.z, q.w},
-                                      reinterpret_cast<u32x4*>(vo + (int64_t)u * 16));
+                                      reinterpret_cast<u32x4*>(vo + off));
         } else {
-          *reinterpret_cast<uint4*>(ko + (int64_t)u * 16) = a;
-          *reinterpret_cast<uint4*>(vo + (int64_t)u * 16) = q;
+          *reinterpret_cast<uint4*>(ko + off) = a;
+          *reinterpret_cast<uint4*>(vo + off) = q;
         }
       }
     }

@@ -95,15 +95,21 @@ __device__ __forceinline__ uint32_t f32x2_to_bf16x2_hw(float lo, float hi) {
 // positive, 0x8000 - mag for negative values (+-0 -> 0x8000), every NaN -> 0xFFFF; desc = ~k.
 // Same order and the same ties as key_bf16 (PyTorch's comparators), not the same codes: use it
 // for every key of a row or for none.
-__device__ __forceinline__ uint32_t key_bf16x2(uint32_t w, bool desc) {
+// key_h16x2: any 16-bit format whose NaNs are the magnitudes above inf_bits (bf16 0x7F80,
+// fp16 0x7C00).
+__device__ __forceinline__ uint32_t key_h16x2(uint32_t w, bool desc, uint32_t inf_bits) {
   typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
   const u16x2 b = __builtin_bit_cast(u16x2, w);
   const u16x2 mag = b & (u16x2)0x7FFF;
   const u16x2 neg = (u16x2)0 - (b >> 15);                      // 0xFFFF where negative
-  const u16x2 nan = (u16x2)0 - ((mag + (u16x2)0x7F) >> 15);    // 0xFFFF where mag > 0x7F80
+  const u16x2 nan =                                            // 0xFFFF where mag > inf_bits
+      (u16x2)0 - ((mag + (u16x2)(unsigned short)(0x7FFFu - inf_bits)) >> 15);
   u16x2 k = ((u16x2)0x8000 + ((mag ^ neg) - neg)) | nan;       // 0x8000 +- mag (mod 2^16)
   if (desc) k = ~k;
   return __builtin_bit_cast(uint32_t, k);
+}
+__device__ __forceinline__ uint32_t key_bf16x2(uint32_t w, bool desc) {
+  return key_h16x2(w, desc, 0x7F80u);
 }
 
 // Sort keys.  Ascending base order is PyTorch's asc comparator
