@@ -489,9 +489,14 @@ __device__ __forceinline__ void snapkv_keys16(const char* nrow, int n, int pool_
                               uint64_t* stamps = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nvec = (n + 7) >> 3;
+  constexpr uint32_t kInf = DT == KVC_BF16 ? 0x7F80u : 0x7C00u;
   uint4 raw[MAXV];
   float mx = -__builtin_huge_valf();
-  int has_nan = 0;
+  // Branch-free local max: the NaN-ignoring float max (v_max_f32) of every element, NaN
+  // detected apart as the packed-u16 max magnitude above inf.  Positions past n read as -inf.
+  // (A signed zero max is harmless: m = dt(max + 1e-6) is the same for -0 and +0.)
+  typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+  u16x2 mag = (u16x2)0;
 #pragma unroll
   for (int q = 0; q < MAXV; ++q) {
     const int v = tid + q * NT;
@@ -502,20 +507,21 @@ __device__ __forceinline__ void snapkv_keys16(const char* nrow, int n, int pool_
     const int v = tid + q * NT;
     const uint32_t w[4] = {raw[q].x, raw[q].y, raw[q].z, raw[q].w};
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const uint32_t u = (w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
-      const float f = in16<DT>(u);
-      if (v < nvec && v * 8 + e < n) {
-        if (f != f) has_nan = 1;
-        else if (f > mx) mx = f;
-      }
+    for (int h = 0; h < 4; ++h) {
+      const int i0 = v * 8 + 2 * h;
+      const uint32_t ninf = 0x8000u | kInf;  // -inf
+      const uint32_t x = i0 + 1 < n ? w[h] : i0 < n ? (w[h] & 0xFFFFu) | (ninf << 16)
+                                                     : ninf | (ninf << 16);
+      mx = __builtin_fmaxf(mx, __builtin_fmaxf(in16<DT>(x & 0xFFFFu), in16<DT>(x >> 16)));
+      mag = __builtin_elementwise_max(mag, __builtin_bit_cast(u16x2, x & 0x7FFF7FFFu));
     }
   }
+  int has_nan = (mag.x > kInf || mag.y > kInf) ? 1 : 0;
   KVC_STAMP(26);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     const float y = __shfl_xor(mx, o, 64);
-    mx = y > mx ? y : mx;
+    mx = __builtin_fmaxf(mx, y);
     has_nan |= __shfl_xor(has_nan, o, 64);
   }
   if (lane == 0) {
@@ -526,7 +532,7 @@ __device__ __forceinline__ void snapkv_keys16(const char* nrow, int n, int pool_
   mx = sc.fmax[0];
   has_nan = sc.fnan[0];
   for (int w = 1; w < NT / 64; ++w) {
-    mx = sc.fmax[w] > mx ? sc.fmax[w] : mx;
+    mx = __builtin_fmaxf(mx, sc.fmax[w]);
     has_nan |= sc.fnan[w];
   }
   if (has_nan) mx = __builtin_nanf("");

@@ -10,7 +10,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ["KVC_LIB"] = os.path.join(ROOT, "cs3602-llm-inference-acceleration_amd", "kvcompress",
-                                     "_lib", "libkvc_stamps.so")
+                                     "_lib", os.environ.get("SEL_LIB", "libkvc_stamps.so"))
 sys.path.insert(0, os.path.join(ROOT, "cs3602-llm-inference-acceleration_amd"))
 from kvcompress import _native as N  # noqa: E402
 
