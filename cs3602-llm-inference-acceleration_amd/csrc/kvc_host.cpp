@@ -91,23 +91,13 @@ py::object scan(py::list kv) {
   return std::move(sig);
 }
 
-// Replays a recorded call on a list that scan() matched to it.
-//   actions : int64 [L, 3] -- (0, -, -) the input pair itself; (1, start, len) K/V[:, :, start:
-//             start+len] (views); (2, job, -) the engine outputs of table row `job`
-//   table   : address of the planned kvc_layer_t rows (pointer columns are filled here), count
-//   n_outs  : output rows of each table row
-//   params  : address of the kvc_params_t the plan was made with
-py::list run(py::list kv, py::array_t<int64_t, py::array::c_style> actions, int64_t table_addr,
-             int64_t n_jobs, std::vector<int64_t> n_outs, int64_t params_addr, int64_t ws,
-             int64_t ws_bytes, int64_t stream) {
-  const Py_ssize_t L = PyList_GET_SIZE(kv.ptr());
-  auto act = actions.unchecked<2>();
-  if (act.shape(0) != L || act.shape(1) != 3 || (int64_t)n_outs.size() != n_jobs)
-    throw std::invalid_argument("kvc_host.run: recorded call does not match the layer list");
-  std::vector<at::Tensor> ks(L), vs(L);
-  for (Py_ssize_t i = 0; i < L; ++i)
-    if (!layer_of(PyList_GET_ITEM(kv.ptr(), i), ks[i], vs[i]))
-      throw std::invalid_argument("kvc_host.run: layer is not a (K, V) pair");
+// Outputs, table pointers, kvc_launch and the result list of a recorded call (run / run_h2o).
+py::list launch_and_list(PyObject* kv, const std::vector<at::Tensor>& ks,
+                         const std::vector<at::Tensor>& vs,
+                         const py::detail::unchecked_reference<int64_t, 2>& act, int64_t table_addr,
+                         int64_t n_jobs, const std::vector<int64_t>& n_outs, int64_t params_addr,
+                         int64_t ws, int64_t ws_bytes, int64_t stream) {
+  const Py_ssize_t L = PyList_GET_SIZE(kv);
   std::vector<at::Tensor> ko(n_jobs), vo(n_jobs);
   if (n_jobs > 0) {
     const at::Tensor& k0 = ks[0];
@@ -132,7 +122,7 @@ py::list run(py::list kv, py::array_t<int64_t, py::array::c_style> actions, int6
     for (Py_ssize_t i = 0; i < L; ++i) {
       if (act(i, 0) != 2) continue;
       const int64_t j = act(i, 1);
-      if (j < 0 || j >= n_jobs) throw std::invalid_argument("kvc_host.run: bad job index");
+      if (j < 0 || j >= n_jobs) throw std::invalid_argument("kvc_host: bad job index");
       table[j].k = ks[i].data_ptr();
       table[j].v = vs[i].data_ptr();
       table[j].k_out = ko[j].data_ptr();
@@ -148,7 +138,7 @@ py::list run(py::list kv, py::array_t<int64_t, py::array::c_style> actions, int6
   for (Py_ssize_t i = 0; i < L; ++i) {
     const int64_t a = act(i, 0);
     if (a == 0) {
-      out[i] = py::reinterpret_borrow<py::object>(PyList_GET_ITEM(kv.ptr(), i));
+      out[i] = py::reinterpret_borrow<py::object>(PyList_GET_ITEM(kv, i));
     } else if (a == 1) {
       const int64_t s = act(i, 1), len = act(i, 2);
       out[i] = py::make_tuple(ks[i].slice(2, s, s + len), vs[i].slice(2, s, s + len));
@@ -160,8 +150,170 @@ py::list run(py::list kv, py::array_t<int64_t, py::array::c_style> actions, int6
   return out;
 }
 
+void unpack_layers(PyObject* kv, std::vector<at::Tensor>& ks, std::vector<at::Tensor>& vs) {
+  const Py_ssize_t L = PyList_GET_SIZE(kv);
+  ks.resize(L);
+  vs.resize(L);
+  for (Py_ssize_t i = 0; i < L; ++i)
+    if (!layer_of(PyList_GET_ITEM(kv, i), ks[i], vs[i]))
+      throw std::invalid_argument("kvc_host: layer is not a (K, V) pair");
+}
+
+// Replays a recorded call on a list that scan() matched to it.
+//   actions : int64 [L, 3] -- (0, -, -) the input pair itself; (1, start, len) K/V[:, :, start:
+//             start+len] (views); (2, job, -) the engine outputs of table row `job`
+//   table   : address of the planned kvc_layer_t rows (pointer columns are filled here), count
+//   n_outs  : output rows of each table row
+//   params  : address of the kvc_params_t the plan was made with
+py::list run(py::list kv, py::array_t<int64_t, py::array::c_style> actions, int64_t table_addr,
+             int64_t n_jobs, std::vector<int64_t> n_outs, int64_t params_addr, int64_t ws,
+             int64_t ws_bytes, int64_t stream) {
+  const Py_ssize_t L = PyList_GET_SIZE(kv.ptr());
+  auto act = actions.unchecked<2>();
+  if (act.shape(0) != L || act.shape(1) != 3 || (int64_t)n_outs.size() != n_jobs)
+    throw std::invalid_argument("kvc_host.run: recorded call does not match the layer list");
+  std::vector<at::Tensor> ks, vs;
+  unpack_layers(kv.ptr(), ks, vs);
+  return launch_and_list(kv.ptr(), ks, vs, act, table_addr, n_jobs, n_outs, params_addr, ws,
+                         ws_bytes, stream);
+}
+
+// ---- h2o_attention (reference kvcompress/methods/h2o_attention.py:84-363) ---------------------
+// A decode step of h2o_attention_compress with a manager is three engine calls: accumulate the
+// new attention rows (:84-153), the heavy hitters of every layer (:156-213) written into the
+// index region of a shared-index gather plan, and that gather (:305-361).  For a repeated call
+// shape the tables are fixed up to their pointers; kvcompress/methods/h2o_attention.py plans
+// them and these two functions key and replay them.
+
+// Memo key of (kv, attention, accumulated) -- scan(kv), then per attention layer (dtype, B, H, q,
+// k, strides 0..2, device) or -1 when it is None, then per accumulated tensor (dtype, shape,
+// device) or -1 -- or None when an input needs the Python path (a layer that is not a plain
+// tensor pair, an attention row that is not last-dim contiguous and element aligned, a
+// non-contiguous accumulated tensor).
+py::object scan_h2o(py::list kv, py::object attns, py::list accs) {
+  py::object base = scan(kv);
+  if (base.is_none()) return py::none();
+  PyObject* seq = PySequence_Fast(attns.ptr(), "attention_scores must be a sequence");
+  if (!seq) throw py::error_already_set();
+  py::object hold = py::reinterpret_steal<py::object>(seq);
+  const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+  if (PyList_GET_SIZE(accs.ptr()) != n) return py::none();
+  std::vector<int64_t> sig;
+  sig.reserve(n * 15);
+  at::Tensor t;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* o = PySequence_Fast_GET_ITEM(seq, i);
+    if (o == Py_None) {
+      sig.push_back(-1);
+      continue;
+    }
+    if (!as_tensor(o, t) || t.dim() != 4 || !t.is_cuda() || dtype_code(t) < 0 ||
+        t.stride(3) != 1 || reinterpret_cast<uintptr_t>(t.data_ptr()) % t.element_size())
+      return py::none();
+    sig.insert(sig.end(), {dtype_code(t), t.size(0), t.size(1), t.size(2), t.size(3),
+                           t.stride(0), t.stride(1), t.stride(2), (int64_t)t.get_device()});
+  }
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    PyObject* o = PyList_GET_ITEM(accs.ptr(), i);
+    if (o == Py_None) {
+      sig.push_back(-1);
+      continue;
+    }
+    if (!as_tensor(o, t) || t.dim() != 3 || !t.is_cuda() || !t.is_contiguous())
+      return py::none();
+    sig.insert(sig.end(), {dtype_code(t), t.size(0), t.size(1), t.size(2),
+                           (int64_t)t.get_device()});
+  }
+  py::tuple b = base.cast<py::tuple>();
+  py::tuple out(b.size() + sig.size());
+  for (size_t i = 0; i < b.size(); ++i) out[i] = b[i];
+  for (size_t i = 0; i < sig.size(); ++i) out[b.size() + i] = py::int_(sig[i]);
+  return std::move(out);
+}
+
+// Replays a planned h2o_attention step on inputs scan_h2o() matched to it.
+//   a_layers : attention layer of each kvc_attn_layer_t row of the planned table at a_table (the
+//              pointer columns are filled here: attn, acc_old of rows with old_len > 0, and
+//              acc_new -- views of one fresh allocation, returned)
+//   hh_rows  : accumulate row whose acc_new each kvc_hh_layer_t row of hh_table reads
+//   idx, idx_stride : the gather plan's index region, where kvc_heavy_hitters writes
+//   the rest : as run()
+// Returns (result list, [acc_new of each accumulate row]).
+py::tuple run_h2o(py::list kv, py::object attns, py::list accs, std::vector<int64_t> a_layers,
+                  int64_t a_table, int64_t a_params, std::vector<int64_t> hh_rows,
+                  int64_t hh_table, int64_t hh_ws, int64_t hh_ws_bytes, int64_t idx,
+                  int64_t idx_stride, py::array_t<int64_t, py::array::c_style> actions,
+                  int64_t table_addr, int64_t n_jobs, std::vector<int64_t> n_outs,
+                  int64_t params_addr, int64_t ws, int64_t ws_bytes, int64_t stream) {
+  const Py_ssize_t L = PyList_GET_SIZE(kv.ptr());
+  auto act = actions.unchecked<2>();
+  if (act.shape(0) != L || act.shape(1) != 3 || (int64_t)n_outs.size() != n_jobs ||
+      a_layers.empty())
+    throw std::invalid_argument("kvc_host.run_h2o: recorded call does not match the inputs");
+  PyObject* seq = PySequence_Fast(attns.ptr(), "attention_scores must be a sequence");
+  if (!seq) throw py::error_already_set();
+  py::object hold = py::reinterpret_steal<py::object>(seq);
+  const Py_ssize_t n_att = PySequence_Fast_GET_SIZE(seq);
+  const size_t na = a_layers.size();
+  std::vector<kvc_attn_layer_t> at(na);
+  std::memcpy(at.data(), reinterpret_cast<const void*>(a_table), sizeof(kvc_attn_layer_t) * na);
+  std::vector<at::Tensor> att(na);
+  int64_t total = 0;
+  for (size_t r = 0; r < na; ++r) {
+    const int64_t li = a_layers[r];
+    if (li < 0 || li >= n_att || !as_tensor(PySequence_Fast_GET_ITEM(seq, li), att[r]))
+      throw std::invalid_argument("kvc_host.run_h2o: attention layer is not a tensor");
+    total += att[r].size(0) * att[r].size(1) * (int64_t)at[r].key_len;
+  }
+  at::Tensor buf = at::empty({total}, att[0].options());
+  py::list acc_out(na);
+  std::vector<at::Tensor> acc_new(na);
+  int64_t off = 0;
+  at::Tensor old;
+  for (size_t r = 0; r < na; ++r) {
+    const int64_t B = att[r].size(0), H = att[r].size(1), k = at[r].key_len;
+    acc_new[r] = buf.as_strided({B, H, k}, {H * k, k, 1}, off);
+    off += B * H * k;
+    at[r].attn = att[r].data_ptr();
+    at[r].acc_new = acc_new[r].data_ptr();
+    at[r].acc_old = nullptr;
+    if (at[r].old_len > 0) {
+      if (!as_tensor(PyList_GET_ITEM(accs.ptr(), a_layers[r]), old))
+        throw std::invalid_argument("kvc_host.run_h2o: accumulated attention missing");
+      at[r].acc_old = old.data_ptr();
+    }
+    acc_out[r] = acc_new[r];
+  }
+  int rc = kvc_attn_accumulate(reinterpret_cast<const kvc_attn_params_t*>(a_params), at.data(),
+                               (int)na, reinterpret_cast<kvc_stream_t>(stream));
+  if (rc != KVC_OK)
+    throw std::runtime_error(std::string("kvc_attn_accumulate failed: ") + kvc_status_string(rc));
+  const size_t nh = hh_rows.size();
+  std::vector<kvc_hh_layer_t> ht(nh);
+  std::memcpy(ht.data(), reinterpret_cast<const void*>(hh_table), sizeof(kvc_hh_layer_t) * nh);
+  for (size_t j = 0; j < nh; ++j) {
+    if (hh_rows[j] < 0 || hh_rows[j] >= (int64_t)na)
+      throw std::invalid_argument("kvc_host.run_h2o: bad heavy-hitter row");
+    ht[j].acc = acc_new[hh_rows[j]].data_ptr();
+  }
+  rc = kvc_heavy_hitters(reinterpret_cast<const kvc_attn_params_t*>(a_params), ht.data(), (int)nh,
+                         reinterpret_cast<int32_t*>(idx), idx_stride,
+                         reinterpret_cast<void*>(hh_ws), (size_t)hh_ws_bytes,
+                         reinterpret_cast<kvc_stream_t>(stream));
+  if (rc != KVC_OK)
+    throw std::runtime_error(std::string("kvc_heavy_hitters failed: ") + kvc_status_string(rc));
+  std::vector<at::Tensor> ks, vs;
+  unpack_layers(kv.ptr(), ks, vs);
+  py::list out = launch_and_list(kv.ptr(), ks, vs, act, table_addr, n_jobs, n_outs, params_addr,
+                                 ws, ws_bytes, stream);
+  return py::make_tuple(out, acc_out);
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "kvcompress native host path (scan / run of a recorded compress call)";
   m.def("scan", &scan, "memo key of a plain (K, V) layer list, or None");
   m.def("run", &run, "replay a recorded compress call: one kvc_launch, outputs, result list");
+  m.def("scan_h2o", &scan_h2o, "memo key of an h2o_attention step's inputs, or None");
+  m.def("run_h2o", &run_h2o, "replay a planned h2o_attention step: accumulate, heavy hitters, "
+        "gather");
 }

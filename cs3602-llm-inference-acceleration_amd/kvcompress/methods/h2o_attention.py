@@ -185,10 +185,16 @@ def h2o_attention_compress(past_key_values, attention_scores: Optional[Tuple] = 
                            start_size: int = 4, heavy_hitter_size: int = 64,
                            recent_size: int = 444, skip_layers: List[int] = [],
                            **kwargs) -> List[Tuple[torch.Tensor, torch.Tensor]]:
-    """h2o_attention.py:216-363."""
+    """h2o_attention.py:216-363.  A repeated decode-step shape with a manager is replayed by the
+    native host path (_replay_step); everything else runs the per-layer logic below."""
     past_key_values = list(normalize_kv_cache(past_key_values))
     if not past_key_values:
         return past_key_values
+    if h2o_manager is not None and attention_scores is not None:
+        out = _replay_step(past_key_values, attention_scores, h2o_manager, start_size,
+                           heavy_hitter_size, recent_size, skip_layers)
+        if out is not None:
+            return out
     total_cache_size = start_size + heavy_hitter_size + recent_size
     if h2o_manager is not None and attention_scores is not None:
         h2o_manager.update_attention_scores(attention_scores, skip_layers)
@@ -276,6 +282,174 @@ def _compact_shared(mgr, jobs, n_hh, out_list):
                 if x is not None:
                     reg[i * B:(i + 1) * B, :x.numel()] = x.to(torch.int32)
     E.execute_shared([s for s, _ in jobs], out_list, fill)
+
+
+# ---------------------------------------------------------------------------------------------
+# Decode steps replayed natively: a repeated (shapes, kwargs, manager settings) step is three
+# engine calls whose tables are fixed up to their pointers (kvc_host.run_h2o)
+# ---------------------------------------------------------------------------------------------
+step_memo = E._PlanCache(capacity=8)
+step_stats = {"replayed": 0, "planned": 0}
+replay_steps = True  # False: every step takes the Python path (tests compare the two)
+
+
+class _StepPlan:
+    __slots__ = ("a_layers", "a_table", "a_params", "hh_rows", "hh_table", "hh_ws", "idx",
+                 "idx_stride", "actions", "table", "n_outs", "params", "ws", "info", "seq_len")
+
+
+def _replay_step(kvl, attention_scores, mgr, start_size, heavy_hitter_size, recent_size,
+                 skip_layers):
+    """The step's outputs from kvc_host.run_h2o, with the manager's state updated as
+    update_attention_scores would, or None when the step takes the Python path (no host module,
+    a timer or recording active, a first sighting, or a shape outside _plan_step's case)."""
+    hm = E.host_module() if replay_steps else None
+    if hm is None or E._timer is not None or E._recording is not None:
+        return None
+    if not isinstance(attention_scores, (tuple, list)):
+        return None
+    accs = [mgr.accumulated_attention.get(i) for i in range(len(attention_scores))]
+    sig = hm.scan_h2o(kvl, attention_scores, accs)
+    if sig is None:
+        return None
+    try:
+        key = (sig, start_size, heavy_hitter_size, recent_size, E._freeze(skip_layers),
+               mgr.start_size, mgr.heavy_hitter_size, mgr.recent_size,
+               float(np.float32(mgr.decay_factor)), mgr._threads(), E.split_select_gather,
+               torch.cuda.current_stream(sig[4]).cuda_stream)
+    except TypeError:
+        return None
+    plan = step_memo.get(key)
+    if plan is None:
+        if not step_memo.admit(key):
+            return None
+        with torch.cuda.device(sig[4]):
+            plan = _plan_step(kvl, attention_scores, accs, mgr, start_size, heavy_hitter_size,
+                              recent_size, skip_layers)
+        if plan is None:
+            return None
+        step_memo.put(key, plan, int(plan.ws.numel()) + int(plan.hh_ws.numel()))
+        step_stats["planned"] += 1
+    step_stats["replayed"] += 1
+    with torch.cuda.device(sig[4]):
+        out, acc = hm.run_h2o(
+            kvl, attention_scores, accs, plan.a_layers, plan.a_table.ctypes.data,
+            E.ctypes_addr(plan.a_params), plan.hh_rows, plan.hh_table.ctypes.data,
+            plan.hh_ws.data_ptr(), int(plan.hh_ws.numel()), plan.idx, plan.idx_stride,
+            plan.actions, plan.table.ctypes.data, len(plan.table), plan.n_outs,
+            E.ctypes_addr(plan.params), plan.ws.data_ptr(), int(plan.info.workspace_bytes),
+            key[-1])
+    for li, a in zip(plan.a_layers, acc):
+        mgr.accumulated_attention[li] = a
+    mgr.current_seq_len = plan.seq_len
+    return out
+
+
+def _plan_step(kvl, attns, accs, mgr, start_size, heavy_hitter_size, recent_size, skip_layers):
+    """Tables of one step -- the same branch logic and arithmetic as update_attention_scores +
+    h2o_attention_compress above, pointer columns left to run_h2o -- for the case where every
+    compressed layer takes its heavy hitters straight from this step's accumulation (batch 1,
+    one attention group, the manager's k equal to the kept count); else None."""
+    L = len(kvl)
+    if len(attns) != L:
+        return None
+    threads = mgr._threads()
+    a_layers, a_rows, acc_len, grp = [], [], {}, None
+    seq_len = mgr.current_seq_len
+    for li, attn in enumerate(attns):  # update_attention_scores (:84-153)
+        if li in skip_layers or attn is None:
+            continue
+        b, h, q, key_len = attn.shape
+        g = (attn.dtype, b, h, attn.get_device())
+        if grp is None:
+            grp = g
+        elif g != grp:
+            return None
+        acc = accs[li]
+        old_len = 0
+        if acc is not None and acc.size(-1) <= key_len:
+            if acc.dtype != attn.dtype or acc.device != attn.device or \
+                    acc.shape[:2] != attn.shape[:2]:
+                return None  # the Python path raises
+            old_len = acc.size(-1)
+        a_layers.append(li)
+        a_rows.append((0, attn.stride()[:3], 0, 0, q, key_len, old_len,
+                       CO.attn_sum_chunk(attn, threads)))
+        acc_len[li] = key_len
+        seq_len = key_len
+    if not a_layers or grp[1] != 1 or grp[3] != kvl[0][0].get_device():
+        return None
+    adt, _, AH, device = grp
+    total_cache_size = start_size + heavy_hitter_size + recent_size
+    actions = np.zeros((L, 3), dtype=np.int64)
+    segs, hh = [], []
+    for layer_idx, (keys, values) in enumerate(kvl):  # h2o_attention_compress (:262-361)
+        S = keys.size(2)
+        if S <= total_cache_size or layer_idx in skip_layers:
+            continue
+        if start_size >= S - recent_size or layer_idx not in acc_len:
+            return None
+        attn_len = acc_len[layer_idx]  # _hh_row
+        m0, m1 = mgr.start_size, min(S, attn_len) - mgr.recent_size
+        if m1 <= m0:
+            return None
+        k = min(mgr.heavy_hitter_size, m1 - m0)
+        sink = E.py_slice(S, None, start_size)[1]
+        t0, tl = E.py_slice(S, -recent_size)
+        z0, zl = E.py_slice(S, start_size, S - recent_size)
+        n_sel = min(k, heavy_hitter_size, zl)
+        if n_sel != k or m1 - m0 > zl:  # not the direct case of _compact_shared
+            return None
+        actions[layer_idx] = (2, len(segs), 0)
+        segs.append((S, z0, zl, n_sel, sink, t0, tl))
+        hh.append((a_layers.index(layer_idx), attn_len, m0, m1 - m0, k,
+                   CO.head_sum_chunk(1, AH, m1 - m0, _esize(adt), threads)))
+    if not segs:
+        return None
+    B, H, _, D = kvl[0][0].shape
+    plan = _StepPlan()
+    plan.a_layers = a_layers
+    plan.a_table = np.array(a_rows, dtype=N.ATTN_LAYER_DTYPE)
+    plan.a_params = _attn_params(adt, 1, AH, mgr.decay_factor, device)
+    plan.hh_rows = [r[0] for r in hh]
+    plan.hh_table = np.zeros(len(hh), dtype=N.HH_LAYER_DTYPE)
+    for i, (_, alen, m0, m, k, chunk) in enumerate(hh):
+        plan.hh_table[i] = (256, alen, m0, m, k, chunk, 0)  # stand-in acc pointer
+    rc, nbytes = N.hh_workspace(plan.a_params, plan.hh_table)
+    N.check(rc, "kvc_hh_workspace")
+    plan.hh_table["acc"] = 0
+    plan.hh_ws = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=keys.device)
+    table = np.zeros(len(segs), dtype=N.LAYER_DTYPE)
+    arr = np.array(segs, dtype=np.int64)
+    S_ = arr[:, 0]
+    st = np.stack([H * S_ * D, S_ * D, np.full_like(S_, D)], axis=1)
+    table["k_stride"] = st
+    table["v_stride"] = st
+    for c, name in enumerate(("seq_len", "zone_start", "zone_len", "n_select", "sink_len",
+                              "tail_start", "tail_len")):
+        table[name] = arr[:, c]
+    for name in ("k", "v", "k_out", "v_out"):
+        table[name] = 256
+    p = E._params(keys.dtype, B, H, D, N.KVC_ASC, N.KVC_ALGO_SORT, True, shared=True)
+    rc, info = N.plan(p, table)
+    N.check(rc, "kvc_plan")
+    if max(r[4] for r in hh) > int(info.index_row_stride):
+        return None
+    for name in ("k", "v", "k_out", "v_out"):
+        table[name] = 0
+    plan.table, plan.params, plan.info = table, p, info
+    plan.n_outs = [int(x) for x in arr[:, 4] + arr[:, 3] + arr[:, 6]]
+    plan.ws = torch.empty(max(int(info.workspace_bytes), 256), dtype=torch.uint8,
+                          device=keys.device)
+    plan.idx = plan.ws.data_ptr() + int(info.index_offset)
+    plan.idx_stride = int(info.index_row_stride)
+    plan.actions = actions
+    plan.seq_len = seq_len
+    return plan
+
+
+def _esize(dtype):
+    return torch.empty(0, dtype=dtype).element_size()
 
 
 def _region_view(ptr, rows, stride, device):

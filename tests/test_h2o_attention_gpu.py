@@ -164,3 +164,64 @@ def test_shared_index_gather_and_index_range_status():
     torch.cuda.synchronize()
     assert int(status.item()) == N.DEV_INDEX_RANGE
     assert torch.equal(ko, k[:, :, want])  # clamped to the zone's last row
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16", "fp16"])
+def test_decode_steps_replayed_natively_match_python_path(dt):
+    """Repeated decode-step shapes go through kvc_host.run_h2o (accumulate, heavy hitters and the
+    shared-index gather from a cached plan): outputs, pass-through objects, the accumulated
+    attention and current_seq_len equal the Python path's step for step, and the accumulated
+    attention equals torch's CPU arithmetic; a shape change is never served by an old plan."""
+    from kvcompress.methods import h2o_attention as HA
+    rng = np.random.default_rng(7)
+    L, H, D, start, hh, recent = 4, 8, 64, 4, 16, 40
+    kw = dict(start_size=start, heavy_hitter_size=hh, recent_size=recent, skip_layers=[1])
+    mk = lambda: HA.H2OAttentionManager(start_size=start, heavy_hitter_size=hh,  # noqa: E731
+                                        recent_size=recent, decay_factor=0.9)
+    mgr_a, mgr_b = mk(), mk()
+    HA.step_memo.clear()
+    r0 = HA.step_stats["replayed"]
+    acc_ref = [None] * L
+    n_steps = 0
+    for step, S in enumerate([61] * 5 + [62] * 3 + [61] * 2):
+        kv = [(to_dev(prng.gen_keys(900 + 10 * step + i, (1, H, S if i != 3 else 30, D), dt)),
+               to_dev(prng.gen_values(900 + 10 * step + i, (1, H, S if i != 3 else 30, D), dt)))
+              for i in range(L)]
+        att_cpu = [_tie_attention(rng, (1, H, 1, S)).to(TORCH_DT[dt]) for _ in range(L)]
+        att = tuple(a.to("cuda:0") for a in att_cpu)
+        out_a = HA.h2o_attention_compress(list(kv), attention_scores=att, h2o_manager=mgr_a, **kw)
+        HA.replay_steps = False
+        try:
+            out_b = HA.h2o_attention_compress(list(kv), attention_scores=att, h2o_manager=mgr_b,
+                                              **kw)
+        finally:
+            HA.replay_steps = True
+        n_steps += 1
+        for li in range(L):
+            assert (out_a[li] is kv[li]) == (out_b[li] is kv[li]), (step, li)
+            for x, y in zip(out_a[li], out_b[li]):
+                assert x.shape == y.shape, (step, li)
+                assert np.array_equal(to_np(x).view(np.uint8), to_np(y).view(np.uint8)), (step, li)
+            if li == 1:  # skipped: never accumulated
+                assert li not in mgr_a.accumulated_attention
+                continue
+            a = mgr_a.accumulated_attention[li]
+            b = mgr_b.accumulated_attention[li]
+            assert np.array_equal(to_np(a).view(np.uint8), to_np(b).view(np.uint8)), (step, li)
+            imp = att_cpu[li].sum(dim=2)
+            r = acc_ref[li]
+            if r is None or r.size(-1) > S:
+                r = torch.zeros(1, H, S, dtype=imp.dtype)
+            elif r.size(-1) < S:
+                r = torch.cat([r * 0.9, torch.zeros(1, H, S - r.size(-1), dtype=imp.dtype)], -1)
+            else:
+                r = r * 0.9
+            acc_ref[li] = r + imp
+            assert np.array_equal(to_np(a).view(np.uint8), to_np(acc_ref[li]).view(np.uint8)), \
+                (step, li)
+        assert mgr_a.current_seq_len == mgr_b.current_seq_len == S
+    # S = 61: steps 0-1 Python (first sightings of two acc shapes), 2-4 replayed; S = 62: 5-6
+    # Python, 7 replayed; back at 61: the acc shape of step 8 is new once more (62 > 61: reset)
+    assert HA.step_stats["replayed"] - r0 >= 5
+    from kvcompress import _engine
+    assert _engine.device_status(0) == 0
