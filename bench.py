@@ -357,6 +357,9 @@ def main():
     ap.add_argument("--dump-layer", default=None, metavar="DIR",
                     help="test only: after the timed region each rank writes its first layer's "
                          "K/V inputs and outputs (heads 0-1) to DIR/rank<r>.npz")
+    ap.add_argument("--dry-run-fail-rank", type=int, default=-1, metavar="R",
+                    help="test only (with --dry-run): rank R exits with an error after joining "
+                         "the process group, before the first barrier")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -378,6 +381,8 @@ def main():
         # MAX / SUM all-reduces of host scalars -- the data path has no exchange, so no RCCL
         import torch.distributed as dist
         dist.init_process_group("gloo")
+    if args.dry_run and rank == args.dry_run_fail_rank:
+        sys.exit(f"rank {rank}: injected failure (--dry-run-fail-rank)")
 
     from kvcompress import _engine
     from kvcompress.methods import get_compress_fn

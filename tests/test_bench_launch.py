@@ -2,13 +2,16 @@
 stand-in step whose last rank is the slow one, no engine and no GPU):
   * `python bench.py --gpus 2` starts two ranks itself and prints ONE JSON line, n_gpus = 2;
   * under torchrun (WORLD_SIZE set) it spawns nothing and reports the same way;
-  * the reported time is the MAX over ranks (the slow rank's).
+  * the reported time is the MAX over ranks (the slow rank's);
+  * a rank that dies after joining the process group ends the whole launch with its error code
+    (the surviving ranks, waiting in a barrier, are stopped) and no JSON line is printed.
 """
 import json
 import os
 import socket
 import subprocess
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STEPS = 5
@@ -78,3 +81,14 @@ def test_strong_scaling_workload_splits_32_layers():
     r, = _json_lines(out.stdout)
     assert r["scaling"] == "strong" and r["config"]["layers_total"] == 32
     assert r["config"]["layers_per_gpu"] == 16
+
+
+def test_rank_failure_after_init_stops_the_launch():
+    t0 = time.time()
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--gpus",
+                          "2", "--steps", str(STEPS), "--warmup", "1", "--dry-run-fail-rank", "1"],
+                         cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert out.returncode != 0
+    assert "injected failure" in out.stderr
+    assert _json_lines(out.stdout) == []
+    assert time.time() - t0 < 120  # rank 0 did not wait out gloo's barrier timeout
