@@ -53,6 +53,8 @@ WORKLOADS = {
                    "cfg4, pythia-2.8b"),
     "snapkv-s16384": ("snapkv_lite", dict(observation_window=32, keep_size=512), 16384, 128,
                       "cfg5, pythia-6.9b"),
+    "snapkv-s4096": ("snapkv_lite", dict(observation_window=32, keep_size=512), 4096, 128,
+                     "cfg5 at the north star's short length"),
     "pyramid-s16384": ("pyramid_kv", dict(base_size=512), 16384, 128, "cfg5, pythia-6.9b"),
     "l2-s16384": ("l2_compress", dict(keep_ratio=0.8, prune_after=100), 16384, 80,
                   "cfg1 method (one-shot), pythia-2.8b"),
