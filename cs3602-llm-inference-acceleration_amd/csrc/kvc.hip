@@ -707,11 +707,85 @@ __device__ __forceinline__ void wave_stable_sort(KeyT* key, uint16_t* idx, int l
 // candidates 64 at a time: element i enters iff key[i] < key[0] at its turn, and key[0] only
 // decreases, so a ballot against the current top leaves exactly the elements the serial loop
 // would pop, in index order (re-checked against the new top after each pop).  The scan of the
-// n - middle elements no longer costs one dependent LDS round trip each.  Call with all 64
-// lanes of one wave; positions >= middle other than the popped one are never written.
+// n - middle elements no longer costs one dependent LDS round trip each.  For middle <= 64 (the
+// h2o heavy hitters' 64) the heap itself lives in the wave's registers (RegHeap) and only its
+// final slots are stored; otherwise lane 0 keeps it in LDS.  Call with all 64 lanes of one wave;
+// the result is the first `middle` positions (positions >= middle are not part of it).
+// The heap of a wave_heap_select with middle <= 64 held in registers: lane j owns heap slot j
+// (key hk, index hi).  std::__adjust_heap + std::__push_heap (kvc_serial.h adjust_heap) with every
+// comparison on readlane'd (wave-uniform) keys and every move a readlane + lane select, so a
+// pop costs no LDS round trips.
+struct RegHeap {
+  uint32_t hk;
+  uint32_t hi;
+  __device__ __forceinline__ uint32_t k(int j) const {
+    return (uint32_t)__builtin_amdgcn_readlane((int)hk, j);
+  }
+  __device__ __forceinline__ void move(int to, int from) {  // slot `to` <- slot `from`
+    set(to, k(from), (uint32_t)__builtin_amdgcn_readlane((int)hi, from));
+  }
+  __device__ __forceinline__ void set(int to, uint32_t vk, uint32_t vi) {
+    const bool me = (int)(threadIdx.x & 63) == to;
+    hk = me ? vk : hk;
+    hi = me ? vi : hi;
+  }
+  __device__ __forceinline__ void adjust(int hole, int len, uint32_t vk, uint32_t vi) {
+    const int top = hole;
+    int second = hole;
+    while (second < (len - 1) / 2) {
+      second = 2 * (second + 1);
+      if (k(second) < k(second - 1)) --second;
+      move(hole, second);
+      hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+      second = 2 * (second + 1);
+      move(hole, second - 1);
+      hole = second - 1;
+    }
+    int parent = (hole - 1) / 2;
+    while (hole > top && k(parent) < vk) {
+      move(hole, parent);
+      hole = parent;
+      parent = (hole - 1) / 2;
+    }
+    set(hole, vk, vi);
+  }
+};
+
 template <typename K, typename I>
 __device__ __forceinline__ void wave_heap_select(K* key, I* idx, int middle, int len) {
   const int lane = threadIdx.x & 63;
+  if (middle <= 64) {  // the heap in registers (RegHeap): make_heap, then the scan with its pops
+    RegHeap h;
+    h.hk = lane < middle ? (uint32_t)key[lane] : 0u;
+    h.hi = lane < middle ? (uint32_t)idx[lane] : 0u;
+    if (middle >= 2)
+      for (int parent = (middle - 2) / 2; parent >= 0; --parent)
+        h.adjust(parent, middle, h.k(parent), (uint32_t)__builtin_amdgcn_readlane((int)h.hi, parent));
+    uint32_t top = h.k(0);
+    for (int base = middle; base < len; base += 64) {
+      const int i = base + lane;
+      const uint32_t ki = i < len ? (uint32_t)key[i] : 0xFFFFFFFFu;
+      const uint32_t ii = i < len ? (uint32_t)idx[i] : 0u;
+      uint64_t cand = __builtin_amdgcn_ballot_w64(i < len && ki < top);
+      while (cand) {
+        const int l = (int)__builtin_ctzll(cand);
+        // std::__pop_heap(first, middle, i): the old top goes to position i (never read again:
+        // only the heap's slots are the result), element i sifts in from the root
+        h.adjust(0, middle, (uint32_t)__builtin_amdgcn_readlane((int)ki, l),
+                 (uint32_t)__builtin_amdgcn_readlane((int)ii, l));
+        top = h.k(0);
+        cand &= ~((2ull << l) - 1ull) & __builtin_amdgcn_ballot_w64(ki < top);
+      }
+    }
+    if (lane < middle) {
+      key[lane] = (K)h.hk;
+      idx[lane] = (I)h.hi;
+    }
+    wave_sync();
+    return;
+  }
   if (lane == 0) make_heap(key, idx, middle);
   wave_sync();
   uint32_t top = (uint32_t)key[0];
