@@ -712,44 +712,44 @@ __device__ __forceinline__ void wave_stable_sort(KeyT* key, uint16_t* idx, int l
 // final slots are stored; otherwise lane 0 keeps it in LDS.  Call with all 64 lanes of one wave;
 // the result is the first `middle` positions (positions >= middle are not part of it).
 // The heap of a wave_heap_select with middle <= 64 held in registers: lane j owns heap slot j
-// (key hk, index hi).  std::__adjust_heap + std::__push_heap (kvc_serial.h adjust_heap) with every
-// comparison on readlane'd (wave-uniform) keys and every move a readlane + lane select, so a
-// pop costs no LDS round trips.
+// (key hk, index hi).  adjust() is std::__adjust_heap + std::__push_heap (kvc_serial.h
+// adjust_heap) computed wave-parallel instead of level by level:
+//   * the down phase moves the hole along the path of "chosen" children (the right child unless
+//     it is strictly smaller than the left; a lone child at (len-2)/2 for even len) to a leaf,
+//     every path node taking its chosen child's entry;
+//   * the up phase moves the value back up while its parent is strictly smaller.  Path keys do
+//     not increase with depth (heap order), so it stops at depth m = #{path nodes below `top`
+//     with !(key < value)}, and its moves undo the down phase below m.
+// Net effect: path depths 0..m-1 take their chosen child's entry, depth m takes the value, the
+// rest of the heap is unchanged.  Each lane derives its chosen child from its children's keys
+// (ds_bpermute), the path is a chase of <= 7 readlanes, and m is one ballot.
 struct RegHeap {
   uint32_t hk;
   uint32_t hi;
   __device__ __forceinline__ uint32_t k(int j) const {
     return (uint32_t)__builtin_amdgcn_readlane((int)hk, j);
   }
-  __device__ __forceinline__ void move(int to, int from) {  // slot `to` <- slot `from`
-    set(to, k(from), (uint32_t)__builtin_amdgcn_readlane((int)hi, from));
-  }
-  __device__ __forceinline__ void set(int to, uint32_t vk, uint32_t vi) {
-    const bool me = (int)(threadIdx.x & 63) == to;
-    hk = me ? vk : hk;
-    hi = me ? vi : hi;
-  }
-  __device__ __forceinline__ void adjust(int hole, int len, uint32_t vk, uint32_t vi) {
-    const int top = hole;
-    int second = hole;
-    while (second < (len - 1) / 2) {
-      second = 2 * (second + 1);
-      if (k(second) < k(second - 1)) --second;
-      move(hole, second);
-      hole = second;
+  __device__ __forceinline__ void adjust(int top, int len, uint32_t vk, uint32_t vi) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int l = min(2 * lane + 1, 63), r = min(2 * lane + 2, 63);
+    const uint32_t kl = (uint32_t)__builtin_amdgcn_ds_bpermute(l * 4, (int)hk);
+    const uint32_t kr = (uint32_t)__builtin_amdgcn_ds_bpermute(r * 4, (int)hk);
+    const uint32_t il = (uint32_t)__builtin_amdgcn_ds_bpermute(l * 4, (int)hi);
+    const uint32_t ir = (uint32_t)__builtin_amdgcn_ds_bpermute(r * 4, (int)hi);
+    const bool two = lane < (len - 1) / 2;                       // both children in the heap
+    const bool lone = (len & 1) == 0 && lane == (len - 2) / 2;   // only the left one
+    const bool left = lone || (two && kr < kl);
+    const int ch = two || lone ? (left ? l : r) : -1;
+    const uint32_t ck = left ? kl : kr, ci = left ? il : ir;
+    int depth = -1;
+    for (int cur = top, d = 0; cur >= 0; ++d) {  // wave-uniform chase, <= log2(len) + 1 steps
+      depth = lane == cur ? d : depth;
+      cur = __builtin_amdgcn_readlane(ch, cur);
     }
-    if ((len & 1) == 0 && second == (len - 2) / 2) {
-      second = 2 * (second + 1);
-      move(hole, second - 1);
-      hole = second - 1;
-    }
-    int parent = (hole - 1) / 2;
-    while (hole > top && k(parent) < vk) {
-      move(hole, parent);
-      hole = parent;
-      parent = (hole - 1) / 2;
-    }
-    set(hole, vk, vi);
+    const int m = __popcll(__builtin_amdgcn_ballot_w64(depth >= 1 && !(hk < vk)));
+    const bool up = depth >= 0 && depth < m, here = depth == m;
+    hk = up ? ck : here ? vk : hk;
+    hi = up ? ci : here ? vi : hi;
   }
 };
 
