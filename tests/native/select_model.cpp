@@ -82,3 +82,80 @@ extern "C" uint32_t model_f32_to_f16(float f) { return kvc::f32_to_f16_rne(f); }
 extern "C" float model_f16_to_f32(uint32_t h) { return kvc::f16_to_f32(h); }
 extern "C" uint32_t model_canon_nan_f16(uint32_t w) { return kvc::canon_nan_f16x2(w); }
 
+
+// ---- the select kernel's register heap (RegHeap in csrc/kvc.hip), 64 lanes simulated ---------
+// adjust() as the kernel computes it: per lane its chosen child from its children's keys, the
+// path from `top` by a chase of chosen children, the stop depth m as a count over path nodes,
+// then path depths < m take their chosen child's entry and depth m the value.  Checked slot by
+// slot against kvc_serial.h's serial adjust_heap (itself checked against libstdc++ above).
+namespace {
+struct ModelRegHeap {
+  uint32_t hk[64] = {0}, hi[64] = {0};
+  void adjust(int top, int len, uint32_t vk, uint32_t vi) {
+    int ch[64], depth[64];
+    uint32_t ck[64], ci[64];
+    for (int lane = 0; lane < 64; ++lane) {
+      const int l = std::min(2 * lane + 1, 63), r = std::min(2 * lane + 2, 63);
+      const bool two = lane < (len - 1) / 2;
+      const bool lone = (len & 1) == 0 && lane == (len - 2) / 2;
+      const bool left = lone || (two && hk[r] < hk[l]);
+      ch[lane] = two || lone ? (left ? l : r) : -1;
+      ck[lane] = left ? hk[l] : hk[r];
+      ci[lane] = left ? hi[l] : hi[r];
+      depth[lane] = -1;
+    }
+    for (int cur = top, d = 0; cur >= 0; ++d) {
+      depth[cur] = d;
+      cur = ch[cur];
+    }
+    int m = 0;
+    for (int lane = 0; lane < 64; ++lane) m += depth[lane] >= 1 && !(hk[lane] < vk);
+    for (int lane = 0; lane < 64; ++lane) {
+      const bool up = depth[lane] >= 0 && depth[lane] < m, here = depth[lane] == m;
+      hk[lane] = up ? ck[lane] : here ? vk : hk[lane];
+      hi[lane] = up ? ci[lane] : here ? vi : hi[lane];
+    }
+  }
+};
+uint64_t splitmix(uint64_t& s) {
+  uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+}  // namespace
+
+// Random rows (n up to 3000, 1..`levels` distinct keys: tie-heavy for small values), every
+// middle 1..64: the register heap's make_heap + scan + pops against kvc_serial.h heap_select,
+// compared slot by slot (key and index).  Returns the number of mismatching rows.
+extern "C" int model_regheap_check(uint64_t seed, int cases) {
+  int bad = 0;
+  for (int c = 0; c < cases; ++c) {
+    const int n = 2 + (int)(splitmix(seed) % 3000);
+    const int middle = 1 + (int)(splitmix(seed) % std::min(64, n - 1));
+    const uint32_t levels = 1 + (uint32_t)(splitmix(seed) % (c % 3 == 0 ? 4 : 65536));
+    std::vector<uint32_t> key(n), idx(n);
+    for (int i = 0; i < n; ++i) {
+      key[i] = (uint32_t)(splitmix(seed) % levels);
+      idx[i] = (uint32_t)i;
+    }
+    std::vector<uint32_t> sk = key, si = idx;
+    kvc::heap_select(sk.data(), si.data(), middle, n);
+    ModelRegHeap h;
+    for (int j = 0; j < middle; ++j) {
+      h.hk[j] = key[j];
+      h.hi[j] = idx[j];
+    }
+    if (middle >= 2)
+      for (int parent = (middle - 2) / 2; parent >= 0; --parent)
+        h.adjust(parent, middle, h.hk[parent], h.hi[parent]);
+    for (int i = middle; i < n; ++i)
+      if (key[i] < h.hk[0]) h.adjust(0, middle, key[i], idx[i]);
+    for (int j = 0; j < middle; ++j)
+      if (h.hk[j] != sk[j] || h.hi[j] != si[j]) {
+        ++bad;
+        break;
+      }
+  }
+  return bad;
+}

@@ -174,3 +174,12 @@ def test_fp16_keys_conversions_and_nan_quieting(model):
         def q(h):
             return h | 0x200 if (h & 0x7FFF) > 0x7C00 else h
         assert model.model_canon_nan_f16(w) == (q(lo) | (q(hi) << 16))
+
+
+def test_register_heap_matches_serial_heap_select(model):
+    """The select kernel's wave-parallel register heap (k <= 64: h2o_attention's heavy hitters)
+    leaves exactly the heap libstdc++'s __heap_select leaves, slot by slot, on 6 000 random rows
+    (a third of them with at most 4 distinct keys)."""
+    model.model_regheap_check.restype = ctypes.c_int
+    model.model_regheap_check.argtypes = [ctypes.c_uint64, ctypes.c_int]
+    assert model.model_regheap_check(12345, 6000) == 0
