@@ -291,6 +291,7 @@ def _compact_shared(mgr, jobs, n_hh, out_list):
 step_memo = E._PlanCache(capacity=8)
 step_stats = {"replayed": 0, "planned": 0}
 replay_steps = True  # False: every step takes the Python path (tests compare the two)
+_NO_PLAN = object()  # step_memo entry of a shape that stays on the Python path
 
 
 class _StepPlan:
@@ -320,6 +321,8 @@ def _replay_step(kvl, attention_scores, mgr, start_size, heavy_hitter_size, rece
     except TypeError:
         return None
     plan = step_memo.get(key)
+    if plan is _NO_PLAN:  # a shape _plan_step does not cover: the Python path, unplanned
+        return None
     if plan is None:
         if not step_memo.admit(key):
             return None
@@ -327,6 +330,7 @@ def _replay_step(kvl, attention_scores, mgr, start_size, heavy_hitter_size, rece
             plan = _plan_step(kvl, attention_scores, accs, mgr, start_size, heavy_hitter_size,
                               recent_size, skip_layers)
         if plan is None:
+            step_memo.put(key, _NO_PLAN, 0)
             return None
         step_memo.put(key, plan, int(plan.ws.numel()) + int(plan.hh_ws.numel()))
         step_stats["planned"] += 1

@@ -223,5 +223,24 @@ def test_decode_steps_replayed_natively_match_python_path(dt):
     # S = 61: steps 0-1 Python (first sightings of two acc shapes), 2-4 replayed; S = 62: 5-6
     # Python, 7 replayed; back at 61: the acc shape of step 8 is new once more (62 > 61: reset)
     assert HA.step_stats["replayed"] - r0 >= 5
+    # a shape the plan does not cover (layer 2 compresses with the accumulation of an earlier
+    # step: its attention is None now) stays on the Python path, call after call
+    r1 = HA.step_stats["replayed"]
+    for step in range(4):
+        kv = [(to_dev(prng.gen_keys(700 + 10 * step + i, (1, H, 61, D), dt)),
+               to_dev(prng.gen_values(700 + 10 * step + i, (1, H, 61, D), dt))) for i in range(L)]
+        att = tuple(None if i == 2 else _tie_attention(rng, (1, H, 1, 61)).to(TORCH_DT[dt]).to("cuda:0")
+                    for i in range(L))
+        out_a = HA.h2o_attention_compress(list(kv), attention_scores=att, h2o_manager=mgr_a, **kw)
+        HA.replay_steps = False
+        try:
+            out_b = HA.h2o_attention_compress(list(kv), attention_scores=att, h2o_manager=mgr_b,
+                                              **kw)
+        finally:
+            HA.replay_steps = True
+        for li in range(L):
+            for x, y in zip(out_a[li], out_b[li]):
+                assert np.array_equal(to_np(x).view(np.uint8), to_np(y).view(np.uint8)), (step, li)
+    assert HA.step_stats["replayed"] == r1
     from kvcompress import _engine
     assert _engine.device_status(0) == 0
