@@ -226,12 +226,7 @@ __device__ __forceinline__ void accum_chunk(float (&acc)[8], const uint4 x, int 
 
 // 16-B chunks of a token row staged per phase: 4 (64-B rows), 8 (multiples of 128 B), 10 (160 B
 // multiples); a row of NC chunks takes NC / CP phases.
-__host__ __device__ constexpr int score_cp(int nc, int dt = KVC_BF16) {
-#ifdef KVC_F16_CP4
-  if (dt == KVC_F16 && nc % 8 == 0) return 4;
-#endif
-  return nc == 4 ? 4 : (nc % 8 == 0 ? 8 : 10);
-}
+__host__ __device__ constexpr int score_cp(int nc) { return nc == 4 ? 4 : (nc % 8 == 0 ? 8 : 10); }
 // padded LDS row of CP chunks: an odd number of 16-B granules keeps every lane's ds_read_b128 of
 // its own token row conflict-free
 __host__ __device__ constexpr int score_rowb(int cp) { return (cp + (cp % 2 == 0 ? 1 : 2)) * 16; }
@@ -240,10 +235,7 @@ __host__ __device__ constexpr int score_rowb(int cp) { return (cp + (cp % 2 == 0
 // workgroups per CU, 14 waves -- D = 80 score 0.1049 -> 0.1011 ms against three 4-wave ones
 // (12 waves); two 7-wave ones, also 14 waves, 0.1063; 8-wave ones 45% slower); 4 for 64-B
 // rows.  A/B in profiles/r03_j_score_variants_ab.jsonl and r03_l_select_variants.json.
-__host__ __device__ constexpr int score_waves(int nc, int dt = KVC_BF16) {
-#ifdef KVC_F16_CP4
-  if (dt == KVC_F16 && nc % 8 == 0) return 8;
-#endif
+__host__ __device__ constexpr int score_waves(int nc) {
   return score_cp(nc) == 8 ? 8 : score_cp(nc) == 10 ? 2 : 4;
 }
 
@@ -254,7 +246,7 @@ template <int DT, int NC, bool NTL = false>
 __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int tt, int H,
                                            char* wl, char* norms, int64_t norm_stride) {
   constexpr int ESZ = DTypeTraits<DT>::esz;
-  constexpr int CP = score_cp(NC, DT);  // 16-B chunks per token per phase
+  constexpr int CP = score_cp(NC);  // 16-B chunks per token per phase
   constexpr int NPH = NC / CP;
   constexpr int ROWB = score_rowb(CP);  // padded LDS row: conflict-free ds_read_b128 per lane
   const int lane = threadIdx.x & 63;
@@ -319,12 +311,12 @@ __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int t
 }
 
 template <int DT, int NC, bool NTL>
-__global__ void __launch_bounds__(score_waves(NC, DT) * 64)
+__global__ void __launch_bounds__(score_waves(NC) * 64)
     score_kernel(const LayerChunk T, int nl, int H, int64_t tile_base, int64_t chunk_tiles,
                  char* __restrict__ norms, int64_t norm_stride) {
-  constexpr int CP = score_cp(NC, DT);
+  constexpr int CP = score_cp(NC);
   constexpr int ROWB = score_rowb(CP);
-  constexpr int kScoreWaves = score_waves(NC, DT);
+  constexpr int kScoreWaves = score_waves(NC);
   __shared__ __attribute__((aligned(16))) char lds[kScoreWaves][kTile * ROWB];
   const kvc_layer_t* L = T.l;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2402,7 +2394,7 @@ static int with_nc(int nc, F&& f) {
 template <int DT, int NC>
 static int launch_score(const LayerChunk& T, int nl, int H, int64_t tile_base,
                         int64_t chunk_tiles, char* norms, int64_t nstride, hipStream_t s) {
-  constexpr int per_wg = score_waves(NC, DT);  // one tile per wave
+  constexpr int per_wg = score_waves(NC);  // one tile per wave
   const unsigned grid = (unsigned)((chunk_tiles + per_wg - 1) / per_wg);
   return launch_k(score_kernel<DT, NC, true>, dim3(grid), dim3(per_wg * 64), 0, s, T, nl, H,
                   tile_base, chunk_tiles, norms, nstride);
