@@ -2628,6 +2628,11 @@ int kvc_version(void) { return KVC_ABI_VERSION; }
 size_t kvc_layer_struct_size(void) { return sizeof(kvc_layer_t); }
 int kvc_max_zone_len(void) { return kvc::kZoneMaxLong; }
 
+#ifndef KVC_SOURCE_DIGEST
+#define KVC_SOURCE_DIGEST "unknown"
+#endif
+const char* kvc_source_digest(void) { return KVC_SOURCE_DIGEST; }
+
 const char* kvc_status_string(int s) {
   switch (s) {
     case KVC_OK: return "ok";

@@ -70,6 +70,7 @@ class PlanInfo(ctypes.Structure):
 
 
 EXPORTS = ("kvc_version", "kvc_layer_struct_size", "kvc_max_zone_len", "kvc_status_string",
+           "kvc_source_digest",
            "kvc_plan", "kvc_launch", "kvc_compress", "kvc_attn_accumulate", "kvc_hh_workspace",
            "kvc_heavy_hitters")
 
@@ -96,6 +97,8 @@ def lib():
     L.kvc_max_zone_len.restype = i32
     L.kvc_status_string.restype = ctypes.c_char_p
     L.kvc_status_string.argtypes = [i32]
+    L.kvc_source_digest.restype = ctypes.c_char_p
+    L.kvc_source_digest.argtypes = []
     L.kvc_plan.restype = i32
     L.kvc_plan.argtypes = [ctypes.POINTER(Params), vp, i32, ctypes.POINTER(PlanInfo)]
     L.kvc_launch.restype = i32
@@ -114,6 +117,11 @@ def lib():
         raise NativeLibraryError("libkvc.so ABI mismatch; rebuild it")
     _lib = L
     return L
+
+
+def source_digest():
+    """SHA-256 of the sources libkvc.so was built from ("unknown" for variant builds)."""
+    return lib().kvc_source_digest().decode()
 
 
 def status_string(rc):

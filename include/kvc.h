@@ -150,6 +150,10 @@ int kvc_version(void);
 size_t kvc_layer_struct_size(void);
 int kvc_max_zone_len(void);
 const char* kvc_status_string(int status);
+/* SHA-256 (hex) of the sources this library was compiled from (csrc/kvc.hip, csrc/kvc_common.h,
+ * csrc/kvc_serial.h, include/kvc.h, in that order), or "unknown" for builds that do not set it --
+ * lets a caller (and tests/test_abi.py) check that a shipped binary matches its source tree. */
+const char* kvc_source_digest(void);
 
 /* Validates the table, fills the kvc_plan() fields of every layer (host memory) and the
  * workspace layout.  Pure host function. */

@@ -59,6 +59,7 @@ static int plan_checks(void) {
   CHECK(kvc_version() == KVC_ABI_VERSION, "ABI version");
   CHECK(kvc_layer_struct_size() == sizeof(kvc_layer_t), "layer struct size");
   CHECK(kvc_max_zone_len() == (1 << 24), "max zone");
+  CHECK(kvc_source_digest() != NULL && strlen(kvc_source_digest()) > 0, "source digest");
   void* fake = (void*)(uintptr_t)4096; /* kvc_plan never dereferences tensor pointers */
   kvc_layer_t l = layer_of(fake, fake, fake, fake, 32, 16384, 128, 512);
   kvc_params_t p = params_of(32, 128, 0);

@@ -26,6 +26,13 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(L, name), name
 
 
+def test_library_built_from_these_sources():
+    """The loaded libkvc.so was compiled from the sources in this tree (build provenance: a
+    binary that travels to the GPU box with the tree is the one its sources describe)."""
+    import __graft_entry__
+    assert N.source_digest() == __graft_entry__.source_digest()
+
+
 def test_struct_layout():
     L = N.lib()
     assert L.kvc_layer_struct_size() == N.LAYER_DTYPE.itemsize == 136
