@@ -381,7 +381,8 @@ def _plan_step(kvl, attns, accs, mgr, start_size, heavy_hitter_size, recent_size
                        CO.attn_sum_chunk(attn, threads)))
         acc_len[li] = key_len
         seq_len = key_len
-    if not a_layers or grp[1] != 1 or grp[3] != kvl[0][0].get_device():
+    if (not a_layers or grp[1] != 1 or grp[3] != kvl[0][0].get_device() or
+            kvl[0][0].shape[0] != 1):
         return None
     adt, _, AH, device = grp
     total_cache_size = start_size + heavy_hitter_size + recent_size
