@@ -860,9 +860,13 @@ __device__ __forceinline__ void unroll_for(F&& f) {
   }
 }
 
-// P1 of a level: the ge / le counts of one wave's stripe, wave-uniform from the compare ballots
-// (s_bcnt on the scalar unit; no per-lane flag state).  WHOLE: every position of the stripe is
-// below hi (unclamped loads with immediate offsets; rows j >= J of a JM-row body read at most
+// P1 of a level: the ge / le counts of one wave's stripe, counted per lane on the VALU (packed
+// ge | le << 16) and summed once per pass (a 16-lane DPP scan, four readlanes).  Ballot counts
+// (s_bcnt + s_add per row on the scalar unit, which all 32 waves of a CU share) cost the
+// selection 2 % (SELECT_GATHER 0.1525 -> 0.1494 ms at the headline, 0.187 -> 0.183 snapkv,
+// 0.128 -> 0.124 h2o; profiles/r03_zz_valu_counts_ab.jsonl): the kernel is bound by the CU's
+// total issue work and the scalar unit carried the larger share.
+// WHOLE: every position of the stripe is below hi (unclamped loads with immediate offsets; rows j >= J of a JM-row body read at most
 // JM/2 rows past the stripe, inside the selection arrays).  Otherwise loads are clamped and
 // lanes past hi masked off.  Position ch is counted with the key it holds (the pivot value);
 // the caller corrects the owner wave's counts for the virtual median move.
@@ -870,6 +874,7 @@ template <typename KeyT, int JM, bool WHOLE>
 __device__ __forceinline__ void p1_counts(const KeyT* key, int pos0, int J, int hi, uint32_t p,
                                           int& cge, int& cle) {
   constexpr int JB = JM < 16 ? JM : 16;
+  uint32_t pc = 0;  // per-lane counts: ge | le << 16 (at most 64 per lane)
   unroll_for<0, JM / JB>([&](auto bc) {
     constexpr int j0 = decltype(bc)::value * JB;
     if (j0 > 0 && j0 >= J) return;
@@ -889,10 +894,16 @@ __device__ __forceinline__ void p1_counts(const KeyT* key, int pos0, int J, int 
         ge = ge && inb;
         le = le && inb;
       }
-      cge += __popcll(__builtin_amdgcn_ballot_w64(ge));
-      cle += __popcll(__builtin_amdgcn_ballot_w64(le));
+      pc += (ge ? 1u : 0u) + (le ? 0x10000u : 0u);
     });
   });
+  const int rs = row_scan16((int)pc);  // per 16-lane row; the four row totals on the scalar unit
+  const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane(rs, 15) +
+                       (uint32_t)__builtin_amdgcn_readlane(rs, 31) +
+                       (uint32_t)__builtin_amdgcn_readlane(rs, 47) +
+                       (uint32_t)__builtin_amdgcn_readlane(rs, 63);
+  cge += (int)(tot & 0xFFFFu);
+  cle += (int)(tot >> 16);
 }
 
 // P2 of a level, rank window 0: scatter the s and g rank -> position tables for ranks <= cap
