@@ -359,6 +359,10 @@ def main():
     ap.add_argument("--dump-layer", default=None, metavar="DIR",
                     help="test only: after the timed region each rank writes its first layer's "
                          "K/V inputs and outputs (heads 0-1) to DIR/rank<r>.npz")
+    ap.add_argument("--as-shard", default=None, metavar="R/W",
+                    help="tool: a single process runs exactly the layers rank R of a W-rank "
+                         "strong-scaling launch owns (--layers-total or a cfg4/cfg5 workload), "
+                         "e.g. 7/8 = the last 4 of 32 layers: the per-rank cost of the N=W split")
     ap.add_argument("--dry-run-fail-rank", type=int, default=-1, metavar="R",
                     help="test only (with --dry-run): rank R exits with an error after joining "
                          "the process group, before the first barrier")
@@ -391,7 +395,19 @@ def main():
 
     method, kwargs, seq_len, head_dim, what = WORKLOADS[args.workload]
     layers_total = args.layers_total or STRONG_DEFAULT.get(args.workload, 0)
-    if layers_total:
+    shard = None
+    if args.as_shard:
+        if world > 1 or not layers_total:
+            sys.exit("--as-shard: one process, and a strong-scaling split (--layers-total L or "
+                     "a cfg4-/cfg5- workload)")
+        sr, sw = (int(x) for x in args.as_shard.split("/"))
+        if not 0 <= sr < sw:
+            sys.exit(f"--as-shard {args.as_shard}: need 0 <= R < W")
+        shard = (sr, sw)
+    if shard:
+        l0, l1 = shard_layers(layers_total, shard[1], shard[0])
+        total, scaling = layers_total, "strong"
+    elif layers_total:
         l0, l1 = shard_layers(layers_total, world, rank)
         total, scaling = layers_total, "strong"
     else:  # rank r owns layers [32r, 32r + 32) of a 32*N-layer stack
@@ -478,7 +494,7 @@ def main():
                                    f"{n_layers} layers of K,V [1,{H},{seq_len},{head_dim}] per "
                                    f"GPU, one call per step ({what})",
                        "name": args.workload, "layers_per_gpu": n_layers,
-                       "layers_total": total, "seq_len": seq_len, "heads": H,
+                       "layers_total": total, "layer_offset": l0, "seq_len": seq_len, "heads": H,
                        "head_dim": head_dim,
                        "parallelism": f"layers sharded x{world}, no collectives"},
             "roofline": {"bound": "hbm", "kernel": desc,
@@ -497,6 +513,9 @@ def main():
         dump_first_layer(args.dump_layer, rank, l0, layers, step())
     if rank == 0:
         res["tokens_evicted_per_sec"] = ev * world * args.steps / elapsed
+        if shard:
+            res["config"]["as_shard"] = f"rank {shard[0]} of {shard[1]} (layers {l0}-{l1 - 1})"
+            res["n_gpus"] = 1
         if args.dry_run:
             res["dry_run"] = True
         elif not args.no_cpu_baseline and method == "fix_size_l2" and world == 1:  # N=1 only

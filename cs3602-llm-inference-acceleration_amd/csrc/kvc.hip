@@ -2515,6 +2515,44 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
   return rc;
 }
 
+// kvc_debug_select_capacity: the 512-thread SELECT / SELECT_GATHER kernels of one chunk with a
+// caller-chosen zone capacity (the device-side bounds check's test hook)
+static int debug_select_impl(const kvc_params_t* p, const kvc_layer_t* layers, int nl, char* w,
+                             size_t wbytes, int zone_cap, hipStream_t s) {
+  kvc_plan_info_t info;
+  int rc = plan_impl(p, const_cast<kvc_layer_t*>(layers), nl, &info, false);
+  if (rc != KVC_OK) return rc;
+  if (nl < 1 || nl > kArgLayers || zone_cap < kTile || zone_cap > kSmallZone ||
+      zone_cap % kTile || p->external_index ||
+      (p->phases != KVC_PHASE_SELECT && p->phases != (KVC_PHASE_SELECT | KVC_PHASE_GATHER)))
+    return KVC_E_ARG;
+  if (!w || wbytes < info.workspace_bytes) return KVC_E_WORKSPACE;
+  LayerChunk T;
+  memcpy(T.l, layers, (size_t)nl * sizeof(kvc_layer_t));
+  const int H = p->heads, BH = p->batch * p->heads;
+  const char* norms = w + info.norm_offset;
+  int32_t* idx = reinterpret_cast<int32_t*>(w + info.index_offset);
+  const dim3 grid((unsigned)(nl * BH));
+  const int nc = p->head_dim * esize(p->dtype) / 16;
+  return with_dtype(p->dtype, [&](auto dt) {
+    constexpr int DT = decltype(dt)::value;
+    constexpr int KC = DT == KVC_F32 ? KVC_F32 : KVC_BF16;
+    const int ks = (int)sizeof(typename DTypeTraits<KC>::key_t);
+    const int cap = sel_cap(zone_cap, ks, kSmallBudget);
+    const size_t lds = sel_bytes(zone_cap, ks, cap);
+    if (p->phases == KVC_PHASE_SELECT)
+      return launch_k(select_kernel<KC, kSelThreadsSmall>, grid, dim3(kSelThreadsSmall), lds, s,
+                      T, BH, DT, p->order, p->algo, norms, info.norm_row_stride, idx,
+                      info.index_row_stride, kWaveSegSmall, zone_cap, cap,
+                      static_cast<uint64_t*>(nullptr), p->device_status);
+    return with_nc(nc, [&](auto ncv) {
+      return launch_k(select_gather_kernel<KC, kSelThreadsSmall, decltype(ncv)::value>, grid,
+                      dim3(kSelThreadsSmall), lds, s, T, H, BH, DT, p->order, p->algo, norms,
+                      info.norm_row_stride, kWaveSegSmall, zone_cap, cap, p->device_status);
+    });
+  });
+}
+
 // ---- h2o_attention host side ----------------------------------------------------------------
 static int attn_params_check(const kvc_attn_params_t* p) {
   if (!p) return KVC_E_ARG;
@@ -2692,6 +2730,13 @@ int kvc_compress(const kvc_params_t* params, kvc_layer_t* layers, int num_layers
   const int rc = kvc::plan_impl(params, layers, num_layers, &info, true);
   if (rc != KVC_OK) return rc;
   return kvc_launch(params, layers, num_layers, ws, ws_bytes, stream);
+}
+
+int kvc_debug_select_capacity(const kvc_params_t* params, const kvc_layer_t* layers,
+                              int num_layers, void* workspace, size_t workspace_bytes,
+                              int zone_cap, kvc_stream_t stream) {
+  return kvc::debug_select_impl(params, layers, num_layers, static_cast<char*>(workspace),
+                                workspace_bytes, zone_cap, reinterpret_cast<hipStream_t>(stream));
 }
 
 int kvc_attn_accumulate(const kvc_attn_params_t* params, const kvc_attn_layer_t* layers,

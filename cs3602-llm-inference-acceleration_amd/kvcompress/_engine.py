@@ -598,7 +598,8 @@ def _record(kvl, out, launches):
                 (rk.storage_offset() - k.storage_offset()) % st):
             return None
         start = (rk.storage_offset() - k.storage_offset()) // st
-        if not (rv.shape == rk.shape and rv.stride() == v.stride() and
+        if not (rv.untyped_storage().data_ptr() == v.untyped_storage().data_ptr() and
+                rv.shape == rk.shape and rv.stride() == v.stride() and
                 rv.storage_offset() - v.storage_offset() == start * v.stride(2)):
             return None
         acts[i] = (1, start, rk.shape[2])

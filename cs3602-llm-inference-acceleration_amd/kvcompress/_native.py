@@ -72,7 +72,7 @@ class PlanInfo(ctypes.Structure):
 EXPORTS = ("kvc_version", "kvc_layer_struct_size", "kvc_max_zone_len", "kvc_status_string",
            "kvc_source_digest",
            "kvc_plan", "kvc_launch", "kvc_compress", "kvc_attn_accumulate", "kvc_hh_workspace",
-           "kvc_heavy_hitters")
+           "kvc_heavy_hitters", "kvc_debug_select_capacity")
 
 _lib = None
 
@@ -113,6 +113,9 @@ def lib():
     L.kvc_heavy_hitters.restype = i32
     L.kvc_heavy_hitters.argtypes = [ctypes.POINTER(AttnParams), vp, i32, vp, ctypes.c_int64, vp,
                                     ctypes.c_size_t, vp]
+    L.kvc_debug_select_capacity.restype = i32
+    L.kvc_debug_select_capacity.argtypes = [ctypes.POINTER(Params), vp, i32, vp, ctypes.c_size_t,
+                                            i32, vp]
     if L.kvc_version() != ABI_VERSION or L.kvc_layer_struct_size() != LAYER_DTYPE.itemsize:
         raise NativeLibraryError("libkvc.so ABI mismatch; rebuild it")
     _lib = L
@@ -159,3 +162,9 @@ def hh_workspace(params, table):
 def heavy_hitters(params, table, out_ptr, out_stride, ws_ptr, ws_bytes, stream_ptr):
     return lib().kvc_heavy_hitters(ctypes.byref(params), table.ctypes.data, len(table), out_ptr,
                                    out_stride, ws_ptr, ws_bytes, stream_ptr)
+
+
+def debug_select_capacity(params, table, ws_ptr, ws_bytes, zone_cap, stream_ptr):
+    """kvc_debug_select_capacity: the test hook of the device-side selection bounds check."""
+    return lib().kvc_debug_select_capacity(ctypes.byref(params), table.ctypes.data, len(table),
+                                           ws_ptr, ws_bytes, zone_cap, stream_ptr)

@@ -223,9 +223,11 @@ def h2o_attention_compress(past_key_values, attention_scores: Optional[Tuple] = 
         if layer_idx in h2o_manager.accumulated_attention:
             acc = h2o_manager.accumulated_attention[layer_idx]
             row = h2o_manager._hh_row(layer_idx, seq_len)
-            if row is not None and acc.shape[0] == 1:
+            if row is not None and acc.shape[0] == 1 and b == 1:
                 # heavy_indices[:num] (:318-321): the first num of the k ascending indices; the
-                # clamp to the middle (:324) never binds when the manager's middle fits in it
+                # clamp to the middle (:324) never binds when the manager's middle fits in it.
+                # (K/V batch > 1 with a batch-1 accumulation: the reference broadcasts its 1-D
+                # index list over the K/V batch (:327-330) -- the host-index path below does.)
                 seg.n_select = min(row[3], heavy_hitter_size, zl)
                 hh_jobs.append((seg, row))
                 continue

@@ -169,6 +169,17 @@ int kvc_launch(const kvc_params_t* params, const kvc_layer_t* layers, int num_la
 int kvc_compress(const kvc_params_t* params, kvc_layer_t* layers, int num_layers,
                  void* workspace, size_t workspace_bytes, kvc_stream_t stream);
 
+/* Diagnostic entry (tests of the device status channel; no reference counterpart).  Runs the
+ * 512-thread SELECT (params->phases == KVC_PHASE_SELECT) or SELECT_GATHER (KVC_PHASE_SELECT |
+ * KVC_PHASE_GATHER) kernel of a planned table (at most 64 layers) as kvc_launch would, but with
+ * the kernels' zone capacity set to `zone_cap` (a multiple of 64, <= 8192) instead of the
+ * table's longest zone.  A row whose zone is longer than that capacity selects nothing, writes
+ * no index and no K/V output row, and ORs KVC_DEV_SELECT_BOUNDS into params->device_status --
+ * the path a dispatch bug would take.  kvc_launch itself always passes a sufficient capacity. */
+int kvc_debug_select_capacity(const kvc_params_t* params, const kvc_layer_t* layers,
+                              int num_layers, void* workspace, size_t workspace_bytes,
+                              int zone_cap, kvc_stream_t stream);
+
 
 /* ---------------------------------------------------------------------------------------------
  * h2o_attention heavy hitters (reference: kvcompress/methods/h2o_attention.py).  The reference's

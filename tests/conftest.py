@@ -27,3 +27,19 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _device_status_stays_clear(request):
+    """After every GPU test: no engine kernel reported a device-side error (include/kvc.h
+    kvc_device_status -- a selection row over its kernel's capacity, a clamped external index)
+    through the engine's per-device status word.  Tests that provoke one use their own word."""
+    yield
+    if "gpu" not in request.node.keywords:
+        return
+    eng = sys.modules.get("kvcompress._engine")
+    if eng is None:
+        return
+    for dev in list(eng._status_words):
+        bits = eng.device_status(dev, clear=True)
+        assert bits == 0, f"device {dev} status word 0x{bits:x} after {request.node.nodeid}"

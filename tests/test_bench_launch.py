@@ -83,6 +83,47 @@ def test_strong_scaling_workload_splits_32_layers():
     assert r["config"]["layers_per_gpu"] == 16
 
 
+def test_eight_ranks_dry_run():
+    """The driver's N=8 launch shapes (bench.py --gpus 8, and torchrun --nproc-per-node 8):
+    8 gloo ranks, ONE JSON line, the max over ranks (the last rank sleeps 16 ms per step)."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--gpus",
+                          "8", "--steps", str(STEPS), "--warmup", "1"], cwd=ROOT, env=_env(),
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    _check(_json_lines(out.stdout), 8)
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          "--nproc-per-node", "8", "--master-addr", "127.0.0.1", "--master-port",
+                          str(_free_port()), os.path.join(ROOT, "bench.py"), "--dry-run", "--gpus",
+                          "8", "--steps", str(STEPS), "--warmup", "1"], cwd=ROOT, env=_env(),
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    _check(_json_lines(out.stdout), 8)
+
+
+def test_strong_split_over_eight_ranks():
+    """cfg5 over 8 ranks: 4 of the 32 layers each (pyramid_kv's min-size layers on the last)."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--gpus",
+                          "8", "--workload", "cfg5-pyramid-l32", "--steps", str(STEPS),
+                          "--warmup", "1"], cwd=ROOT, env=_env(), capture_output=True, text=True,
+                         timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r, = _json_lines(out.stdout)
+    assert r["scaling"] == "strong" and r["n_gpus"] == 8
+    assert r["config"]["layers_total"] == 32 and r["config"]["layers_per_gpu"] == 4
+
+
+def test_as_shard_runs_one_ranks_layers():
+    """--as-shard 7/8: one process runs the layers rank 7 of an 8-rank strong split owns."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run",
+                          "--workload", "cfg5-pyramid-l32", "--as-shard", "7/8", "--steps",
+                          str(STEPS), "--warmup", "1"], cwd=ROOT, env=_env(), capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    r, = _json_lines(out.stdout)
+    assert r["config"]["layer_offset"] == 28 and r["config"]["layers_per_gpu"] == 4
+    assert r["n_gpus"] == 1 and "rank 7 of 8" in r["config"]["as_shard"]
+
+
 def test_rank_failure_after_init_stops_the_launch():
     t0 = time.time()
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--gpus",

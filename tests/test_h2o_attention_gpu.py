@@ -244,3 +244,28 @@ def test_decode_steps_replayed_natively_match_python_path(dt):
     assert HA.step_stats["replayed"] == r1
     from kvcompress import _engine
     assert _engine.device_status(0) == 0
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_kv_batch_above_attention_batch_broadcasts_indices(dt):
+    """K/V batch 2 with a batch-1 accumulation: the reference's 1-D heavy-hitter list is
+    broadcast over the K/V batch (h2o_attention.py:318-333); checked against torch's CPU ops."""
+    from kvcompress.methods.h2o_attention import H2OAttentionManager, h2o_attention_compress
+    rng = np.random.default_rng(3)
+    H, S, D, start, hh, recent = 8, 300, 64, 4, 16, 40
+    mgr = H2OAttentionManager(start_size=start, heavy_hitter_size=hh, recent_size=recent)
+    mgr.reduction_threads = torch.get_num_threads()
+    attn = _tie_attention(rng, (1, H, 3, S)).to(TORCH_DT[dt])
+    k = torch.from_numpy(rng.standard_normal((2, H, S, D)).astype(np.float32)).to(TORCH_DT[dt])
+    v = torch.from_numpy(rng.standard_normal((2, H, S, D)).astype(np.float32)).to(TORCH_DT[dt])
+    out = h2o_attention_compress([(k.to("cuda:0"), v.to("cuda:0"))] * 2,
+                                 attention_scores=(attn.to("cuda:0"),) * 2, h2o_manager=mgr,
+                                 start_size=start, heavy_hitter_size=hh, recent_size=recent)
+    acc = torch.zeros(1, H, S, dtype=attn.dtype) + attn.sum(dim=2)  # CPU reference ops
+    agg = acc[:, :, start:S - recent].sum(dim=1).squeeze(0)
+    idx = torch.sort(torch.topk(agg, hh, dim=-1)[1])[0]
+    for x, ref in zip(out[0], (k, v)):
+        mid = ref[:, :, start:S - recent]
+        want = torch.cat([ref[:, :, :start], mid[:, :, idx], ref[:, :, -recent:]], dim=2)
+        assert np.array_equal(to_np(x).view(np.uint8), to_np(want).view(np.uint8))
+    assert [x.shape for x in out[1]] == [x.shape for x in out[0]]

@@ -10,6 +10,10 @@
 #   decode     per-token decode steps (tools/decode_bench.py)                   -> decode.json
 #   workloads  every bench.py workload at N=1                                   -> workloads.jsonl
 #   pmc        FETCH/WRITE traffic + SQ counters (tools/pmc_round.sh)
+#   shard      per-rank cost of the N=8 strong split (cfg4 / cfg5 workloads, --as-shard R/8 for
+#              the first and last rank) + a rocprofv3 trace of the last rank's cfg5 pyramid step
+#                                                                               -> shard.jsonl, shardprof/
+#   dtypes     the headline in fp32 and fp16 K/V                                -> dtypes.jsonl
 #   ab         A/B of library builds named in $AB_LIBS (files in kvcompress/_lib) on the
 #              workloads in $AB_WORKLOADS (bench.py, 2 repeats)                   -> ab.jsonl
 # Every GPU step runs under its own time limit and the first failure ends the call.
@@ -54,6 +58,27 @@ for step in "$@"; do
             >> "$O/workloads.jsonl" 2>> "$O/workloads.err" || { tail "$O/workloads.err"; exit 1; }
       done
       cat "$O/workloads.jsonl" ;;
+    shard)
+      : > "$O/shard.jsonl"
+      for w in cfg4-h2o-l32 cfg5-snapkv-l32 cfg5-pyramid-l32; do
+        for r in 0 7; do
+          timeout -k 10 200 python bench.py --workload $w --as-shard $r/8 --steps 50 --warmup 5 \
+              --no-cpu-baseline >> "$O/shard.jsonl" 2>> "$O/shard.err" || { tail "$O/shard.err"; exit 1; }
+        done
+      done
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+          --output-format csv -d "$O/shardprof" -o run -- python3 "$R/bench.py" --workload cfg5-pyramid-l32 \
+          --as-shard 7/8 --steps 50 --warmup 5 --no-cpu-baseline > "$O/shardprof.log" 2>&1 ) \
+          || { tail "$O/shardprof.log"; exit 1; }
+      python3 tools/trace_gaps.py "$(find "$O/shardprof" -name '*kernel_trace.csv' | head -1)" timed > "$O/shard_gaps.json" \
+          && cat "$O/shard.jsonl" "$O/shard_gaps.json" ;;
+    dtypes)
+      : > "$O/dtypes.jsonl"
+      for d in fp32 fp16; do
+        timeout -k 10 200 python bench.py --dtype $d --steps 20 --warmup 5 --no-cpu-baseline \
+            >> "$O/dtypes.jsonl" 2>> "$O/dtypes.err" || { tail "$O/dtypes.err"; exit 1; }
+      done
+      cat "$O/dtypes.jsonl" ;;
     pmc)
       bash tools/pmc_round.sh > "$O/pmc_round.out" 2>&1 || { tail -20 "$O/pmc_round.out"; exit 1; }
       tail -c 3000 "$O/pmc_round.out" ;;

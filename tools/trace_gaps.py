@@ -1,6 +1,8 @@
 """Back-to-back check of a rocprofv3 kernel trace (python trace_gaps.py run_kernel_trace.csv):
 for the engine's kernels (kvc::), the per-kernel average duration and the idle gap between the
-end of one engine kernel and the start of the next, over the LAST half of the trace (warm)."""
+end of one engine kernel and the start of the next, over the LAST half of the trace (warm), or
+with a second argument `timed` over the second tenth to the half of it (bench.py's uninstrumented
+timed pass when its K timed steps are 10x its W warmup steps: the second pass splits launches)."""
 import csv
 import json
 import statistics
@@ -8,7 +10,10 @@ import sys
 
 rows = [r for r in csv.DictReader(open(sys.argv[1])) if "kvc::" in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-rows = rows[len(rows) // 2:]
+if len(sys.argv) > 2 and sys.argv[2] == "timed":
+    rows = rows[len(rows) // 10:len(rows) // 2]
+else:
+    rows = rows[len(rows) // 2:]
 dur, gaps = {}, []
 for a, b in zip(rows, rows[1:]):
     gaps.append((int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1e3)
