@@ -851,6 +851,14 @@ __device__ __forceinline__ int mbcnt(uint64_t mask, int base) {
                                         __builtin_amdgcn_mbcnt_lo((uint32_t)mask, (uint32_t)base));
 }
 
+// Materialises x in a VGPR here: keeps the compiler from sinking the computation of a select
+// operand into an exec-mask branch (s_and_saveexec / s_or_b64 exec: scalar instructions on the
+// CU's one scalar unit, shared by all its waves) when only some lanes use it.
+__device__ __forceinline__ int vreg(int x) {
+  asm("" : "+v"(x));
+  return x;
+}
+
 // f(integral_constant<int, I>) for I in [B, E): a loop the compiler cannot leave rolled.
 template <int B, int E, typename F>
 __device__ __forceinline__ void unroll_for(F&& f) {
@@ -929,6 +937,7 @@ __device__ __forceinline__ void p2_window0(const KeyT* key, uint16_t* spos, uint
   // (profiles/r03_c_p2_keys_in_flight_ab.jsonl)
   constexpr int JB = JM < 8 ? JM : 8;
   const int t1 = tot_le + 1;
+  const int cap1 = cap + 1;  // the dump slot (slots 1..cap are the window's ranks)
   const int g1 = rge1;  // P2_RIGHT: rank of the stripe's first ge position
   int ff = kBig;        // P2_RIGHT: the stripe's first ge position (wave-uniform)
   unroll_for<0, JM / JB>([&](auto bc) {
@@ -951,15 +960,19 @@ __device__ __forceinline__ void p2_window0(const KeyT* key, uint16_t* spos, uint
         ge = inb && (isch ? kge : ge);
         le = inb && (isch ? kle : le);
       }
+      // Scatter slots are plain selects (v_min + v_cndmask): a rank past the window goes to the
+      // never-read slot cap + 1, a lane without the flag to its sink.  (Written as
+      // `flag && rank <= cap ? rank : sink`, the compiler emitted two exec-mask branches per row
+      // of 64 positions -- 7 scalar instructions on the CU's one scalar unit.)
       if constexpr (MODE == P2_LEFT) {
         const uint64_t bg = __builtin_amdgcn_ballot_w64(ge);
-        const int a1 = mbcnt(bg, rge1);
-        gpos[(ge && a1 <= cap) ? a1 : lane - 64] = (uint16_t)pj;
+        const int a1 = vreg(min(mbcnt(bg, rge1), cap1));
+        gpos[ge ? a1 : lane - 64] = (uint16_t)pj;
         rge1 += __popcll(bg);
       } else if constexpr (MODE == P2_RIGHT) {
         const uint64_t bl = __builtin_amdgcn_ballot_w64(le);
-        const int sr = t1 - (mbcnt(bl, rle) + (le ? 1 : 0));
-        spos[(le && sr <= cap) ? sr : lane - 64] = (uint16_t)pj;
+        const int sr = vreg(min(t1 - 1 - mbcnt(bl, rle), cap1));  // s rank of an le position
+        spos[le ? sr : lane - 64] = (uint16_t)pj;
         rle += __popcll(bl);
         if (ff == kBig) {
           const uint64_t bg = __builtin_amdgcn_ballot_w64(ge);
@@ -967,10 +980,10 @@ __device__ __forceinline__ void p2_window0(const KeyT* key, uint16_t* spos, uint
         }
       } else {
         const uint64_t bg = __builtin_amdgcn_ballot_w64(ge), bl = __builtin_amdgcn_ballot_w64(le);
-        const int a1 = mbcnt(bg, rge1);                   // g rank: A + 1
-        const int sr = t1 - (mbcnt(bl, rle) + (le ? 1 : 0));  // s rank: tot_le - Lin + 1
-        spos[(le && sr <= cap) ? sr : lane - 64] = (uint16_t)pj;
-        gpos[(ge && a1 <= cap) ? a1 : lane - 64] = (uint16_t)pj;
+        const int a1 = vreg(mbcnt(bg, rge1));                   // g rank: A + 1
+        const int sr = vreg(t1 - (mbcnt(bl, rle) + (le ? 1 : 0)));  // s rank: tot_le - Lin + 1
+        spos[le ? min(sr, cap1) : lane - 64] = (uint16_t)pj;
+        gpos[ge ? min(a1, cap1) : lane - 64] = (uint16_t)pj;
         // g_t < s_t  <=>  A + Lin < tot_le  <=>  a1 < sr: swapped (a prefix t <= m of the g's)
         nsw += __popcll(bg & __builtin_amdgcn_ballot_w64(a1 < sr));
         rge1 += __popcll(bg);
@@ -1142,22 +1155,29 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
   while (true) {
     // ---- P4: this window's swaps (disjoint pairs g_t <-> s_t), spread evenly over the NT
     // lanes: rank-table loads, then key/idx loads, then stores ----
+    // Lanes past the window's last rank swap the pivot slot lo with itself (lo is never a
+    // swapped g_t or s_t: every g_t > lo, and a swapped s_t > g_t), so the loads and stores need
+    // no exec-mask branches; q-rows with no rank left for the wave are skipped uniformly.
     const int wend = min(msw, wb + cap);
     for (int base = wb + 1; base <= wend; base += NT * 4) {
       if (base + wid * 64 > wend) break;  // no rank left for this wave
+      const int nq = uni(min(4, (wend - base - wid * 64) / NT + 1));  // q-rows with a rank
       int gp[4], sp[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
+        if (q >= nq) break;
         const int t = base + tid + q * NT;
-        const int ti = t <= wend ? t - wb : 0;
+        const bool v = t <= wend;
+        const int ti = v ? t - wb : 0;
         const int g = gpos[ti], sv = spos[ti];
-        gp[q] = t <= wend ? g : lo;
-        sp[q] = t <= wend ? sv : lo;
+        gp[q] = v ? g : lo;
+        sp[q] = v ? sv : lo;
       }
       KeyT kg[4], ks[4];
       uint16_t ig[4], is[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
+        if (q >= nq) break;
         kg[q] = key[gp[q]];
         ks[q] = key[sp[q]];
         ig[q] = idx[gp[q]];
@@ -1165,12 +1185,11 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        if (base + tid + q * NT <= wend) {
-          key[gp[q]] = ks[q];
-          key[sp[q]] = kg[q];
-          idx[gp[q]] = is[q];
-          idx[sp[q]] = ig[q];
-        }
+        if (q >= nq) break;
+        key[gp[q]] = ks[q];
+        key[sp[q]] = kg[q];
+        idx[gp[q]] = is[q];
+        idx[sp[q]] = ig[q];
       }
     }
     if (wend >= msw) break;
@@ -2210,10 +2229,14 @@ constexpr int kColThreads = 256;
 //   imp = dt(0 + sum_q attn[b,h,q,j])                     attn.sum(dim=2)           (:116)
 //   acc_new = dt(base + imp), base = dt(acc_old*decay) for j < old_len, else 0  (:118-151)
 // Reads of attn are coalesced across the block's columns (q rows of stride attn_stride[2]).
-template <int DT>
+// ODT: dtype of acc_old.  ODT != DT (the carried accumulation and the new attention differ in
+// dtype, every layer carried): base is rounded to ODT, and acc_new is fp32 -- torch's promotion
+// of two different float dtypes through torch.cat / + (:129-151) -- holding fp32(base) + fp32(imp).
+template <int DT, int ODT>
 __global__ void __launch_bounds__(kColThreads)
     attn_accum_kernel(const AttnChunk T, int H, int BH, float decay, int group, int vec_min) {
   constexpr int ESZ = DTypeTraits<DT>::esz;
+  constexpr int NDT = ODT == DT ? DT : KVC_F32;  // acc_new's dtype
   const kvc_attn_layer_t* ly = T.l + blockIdx.x / BH;
   const int r = (int)(blockIdx.x % BH);
   const int j = (int)blockIdx.y * kColThreads + (int)threadIdx.x;
@@ -2235,9 +2258,9 @@ __global__ void __launch_bounds__(kColThreads)
   const float imp = round_dt<DT>(s);
   float base = 0.f;
   if (j < ly->old_len)
-    base = round_dt<DT>(load_dt<DT>(static_cast<const char*>(ly->acc_old),
-                                    (int)((int64_t)r * ly->old_len + j)) * decay);
-  store_dt<DT>(ly->acc_new, (int64_t)r * k + j, base + imp);
+    base = round_dt<ODT>(load_dt<ODT>(static_cast<const char*>(ly->acc_old),
+                                      (int)((int64_t)r * ly->old_len + j)) * decay);
+  store_dt<NDT>(ly->acc_new, (int64_t)r * k + j, base + imp);
 }
 
 // get_heavy_hitter_indices' head sum (h2o_attention.py:194-198) for every layer of the chunk:
@@ -2274,9 +2297,13 @@ static inline int esize(int dtype) { return dtype == KVC_F32 ? 4 : 2; }
 // Calls f(std::integral_constant<int, DT>) for the call's storage dtype (validated by plan_impl).
 template <typename F>
 static int with_dtype(int dtype, F&& f) {
+#ifdef KVC_ISA_PROBE  // diagnostic compile for ISA inspection: bf16 instantiations only
+  return dtype == KVC_BF16 ? f(std::integral_constant<int, KVC_BF16>()) : KVC_E_DTYPE;
+#else
   if (dtype == KVC_BF16) return f(std::integral_constant<int, KVC_BF16>());
   if (dtype == KVC_F16) return f(std::integral_constant<int, KVC_F16>());
   return f(std::integral_constant<int, KVC_F32>());
+#endif
 }
 static inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 static inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
@@ -2388,6 +2415,9 @@ static int launch_k(void (*kern)(P...), dim3 grid, dim3 block, size_t lds, hipSt
 // plan_impl: 64..1024-byte rows).
 template <typename F>
 static int with_nc(int nc, F&& f) {
+#ifdef KVC_ISA_PROBE  // D = 128 bf16 rows only
+  return nc == 16 ? f(std::integral_constant<int, 16>()) : KVC_E_HEADDIM;
+#else
   switch (nc) {
     case 4: return f(std::integral_constant<int, 4>());
     case 8: return f(std::integral_constant<int, 8>());
@@ -2398,6 +2428,7 @@ static int with_nc(int nc, F&& f) {
     case 64: return f(std::integral_constant<int, 64>());
     default: return KVC_E_HEADDIM;
   }
+#endif
 }
 
 // Keys are read once (non-temporal loads) and outputs written once (non-temporal stores): they
@@ -2554,10 +2585,13 @@ static int debug_select_impl(const kvc_params_t* p, const kvc_layer_t* layers, i
 }
 
 // ---- h2o_attention host side ----------------------------------------------------------------
-static int attn_params_check(const kvc_attn_params_t* p) {
+static int attn_params_check(const kvc_attn_params_t* p, bool accumulate = false) {
   if (!p) return KVC_E_ARG;
   if (p->dtype != KVC_BF16 && p->dtype != KVC_F16 && p->dtype != KVC_F32) return KVC_E_DTYPE;
-  if (p->batch < 1 || p->heads < 1 || p->flags != 0) return KVC_E_ARG;
+  if (p->batch < 1 || p->heads < 1) return KVC_E_ARG;
+  // flags: kvc_attn_accumulate's KVC_ATTN_OLD_DTYPE(d) only (d a dtype other than p->dtype)
+  if (p->flags != 0 && (!accumulate || (p->flags & ~3) || p->flags == KVC_ATTN_OLD_DTYPE(p->dtype)))
+    return KVC_E_ARG;
   if (p->vec_bytes < 16 || p->vec_bytes > 64 || p->vec_bytes % 16) return KVC_E_ARG;
   if ((int64_t)p->batch * p->heads > 0x7FFFFFFF / kArgLayers) return KVC_E_ARG;
   return KVC_OK;
@@ -2565,15 +2599,18 @@ static int attn_params_check(const kvc_attn_params_t* p) {
 
 static int accumulate_impl(const kvc_attn_params_t* p, const kvc_attn_layer_t* layers, int nl,
                            hipStream_t s) {
-  int rc = attn_params_check(p);
+  int rc = attn_params_check(p, true);
   if (rc != KVC_OK) return rc;
   if (nl < 0 || (nl > 0 && !layers)) return KVC_E_ARG;
   const int es = esize(p->dtype);
+  const int odt = p->flags ? p->flags - 1 : p->dtype;  // acc_old's dtype
+  const int oes = esize(odt), nes = p->flags ? 4 : es;
   for (int l = 0; l < nl; ++l) {
     const kvc_attn_layer_t& y = layers[l];
     if (!y.attn || !y.acc_new || y.q_len < 1 || y.key_len < 1 || y.old_len < 0 ||
         y.old_len > y.key_len || (y.old_len > 0 && !y.acc_old) || y.col_chunk < 0 ||
-        ((uintptr_t)y.attn | (uintptr_t)y.acc_new | (uintptr_t)y.acc_old) % es)
+        (p->flags && y.old_len == 0) || (uintptr_t)y.attn % es ||
+        (uintptr_t)y.acc_new % nes || (uintptr_t)y.acc_old % oes)
       return KVC_E_ARG;
     if ((y.key_len + kColThreads - 1) / kColThreads > 65535) return KVC_E_TOO_LONG;
   }
@@ -2587,8 +2624,10 @@ static int accumulate_impl(const kvc_attn_params_t* p, const kvc_attn_layer_t* l
     for (int l = 0; l < cn; ++l) kmax = T.l[l].key_len > kmax ? T.l[l].key_len : kmax;
     const dim3 grid((unsigned)(cn * BH), (unsigned)((kmax + kColThreads - 1) / kColThreads));
     rc = with_dtype(p->dtype, [&](auto dt) {
-      return launch_k(attn_accum_kernel<decltype(dt)::value>, grid, dim3(kColThreads), 0, s, T,
-                      H, BH, p->decay, group, vec_min);
+      return with_dtype(odt, [&](auto od) {
+        return launch_k(attn_accum_kernel<decltype(dt)::value, decltype(od)::value>, grid,
+                        dim3(kColThreads), 0, s, T, H, BH, p->decay, group, vec_min);
+      });
     });
   }
   return rc;

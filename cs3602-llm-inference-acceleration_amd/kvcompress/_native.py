@@ -20,6 +20,12 @@ KVC_SCORE_NORM, KVC_SCORE_SNAPKV = 0, 1
 PHASE_SCORE, PHASE_SELECT, PHASE_GATHER, PHASE_ALL = 1, 2, 4, 7
 FLAG_SPLIT_SELECT_GATHER, FLAG_SHARED_INDEX = 1, 2
 DEV_SELECT_BOUNDS, DEV_INDEX_RANGE = 1, 2  # enum kvc_device_status bits
+
+
+def ATTN_OLD_DTYPE(d):
+    """kvc_attn_params.flags of kvc_attn_accumulate: acc_old of dtype d (KVC_ATTN_OLD_DTYPE)."""
+    return d + 1
+
 ABI_VERSION = 3
 KVC_E_TOO_LONG = -5
 

@@ -30,9 +30,13 @@ from ..utils import normalize_kv_cache
 _DT = {torch.bfloat16: N.KVC_BF16, torch.float16: N.KVC_F16, torch.float32: N.KVC_F32}
 
 
-def _attn_params(dtype, B, H, decay, device):
+def _attn_params(dtype, B, H, decay, device, old_dtype=None):
+    """old_dtype: the carried accumulations' dtype when it differs from the attention's (torch
+    then promotes to float32, h2o_attention.py:129-151; kvc_attn_accumulate's
+    KVC_ATTN_OLD_DTYPE flag)."""
+    flags = N.ATTN_OLD_DTYPE(_DT[old_dtype]) if old_dtype not in (None, dtype) else 0
     return N.AttnParams(dtype=_DT[dtype], batch=B, heads=H, vec_bytes=CO.SUM_VEC_BYTES,
-                        decay=float(np.float32(decay)), flags=0,
+                        decay=float(np.float32(decay)), flags=flags,
                         device_status=E.status_word(device).data_ptr())
 
 
@@ -76,8 +80,10 @@ class H2OAttentionManager:
 
     def update_attention_scores(self, attentions, skip_layers: List[int] = []):
         """h2o_attention.py:84-153 for every given layer in one engine launch per
-        (device, dtype, B, H) group: acc <- acc*decay (zero-extended to the new key length; reset
-        to zeros if the cache shrank) + attention summed over queries."""
+        (device, dtype, B, H, carried dtype) group: acc <- acc*decay (zero-extended to the new key
+        length; reset to zeros if the cache shrank) + attention summed over queries.  A carried
+        accumulation of another float dtype than the new attention is promoted as torch does
+        (`acc * decay` rounded in its own dtype, the sum in float32, a float32 result: :129-151)."""
         if attentions is None:
             return
         groups = {}
@@ -92,22 +98,26 @@ class H2OAttentionManager:
             acc = self.accumulated_attention.get(layer_idx)
             old = None
             if acc is not None and acc.size(-1) <= key_len:  # decay (and zero-extend) (:124-146)
-                if acc.dtype != attn.dtype or acc.device != attn.device or \
-                        acc.shape[:2] != attn.shape[:2]:
-                    raise NotImplementedError(
-                        f"layer {layer_idx}: accumulated attention {acc.dtype}/{acc.device}/"
-                        f"{tuple(acc.shape)} does not match the new attention "
-                        f"{attn.dtype}/{attn.device}/{tuple(attn.shape)}")
+                _check_gpu(acc, f"accumulated attention of layer {layer_idx}")
+                if acc.device != attn.device:  # torch.cat / + raise the same way
+                    raise RuntimeError(
+                        f"layer {layer_idx}: accumulated attention on {acc.device}, new attention "
+                        f"on {attn.device}: expected all tensors to be on the same device")
+                if acc.shape[:2] != attn.shape[:2]:  # torch.cat raises; + would broadcast
+                    raise RuntimeError(
+                        f"layer {layer_idx}: accumulated attention {tuple(acc.shape)} and new "
+                        f"attention {tuple(attn.shape)} differ in batch / heads (not supported)")
                 old = acc.contiguous()
             # acc.size(-1) > key_len: reset to zeros (:138-144) -- old stays None
-            key = (attn.get_device(), attn.dtype, b, h)
+            key = (attn.get_device(), attn.dtype, b, h, attn.dtype if old is None else old.dtype)
             groups.setdefault(key, []).append(
                 (layer_idx, attn, old, CO.attn_sum_chunk(attn, threads)))
             self.current_seq_len = key_len
-        for (device, dtype, b, h), jobs in groups.items():
+        for (device, dtype, b, h, odt), jobs in groups.items():
             with torch.cuda.device(device):
                 sizes = [b * h * a.size(3) for _, a, _, _ in jobs]
-                buf = torch.empty(sum(sizes), dtype=dtype, device=torch.device("cuda", device))
+                ndt = dtype if odt == dtype else torch.float32  # torch's promotion (:129-151)
+                buf = torch.empty(sum(sizes), dtype=ndt, device=torch.device("cuda", device))
                 accs = [t.view(b, h, a.size(3)) for t, (_, a, _, _) in zip(buf.split(sizes), jobs)]
                 table = np.zeros(len(jobs), dtype=N.ATTN_LAYER_DTYPE)
                 for i, ((li, a, old, chunk), acc) in enumerate(zip(jobs, accs)):
@@ -115,7 +125,7 @@ class H2OAttentionManager:
                                 old.data_ptr() if old is not None else 0, acc.data_ptr(),
                                 a.size(2), a.size(3), old.size(-1) if old is not None else 0,
                                 chunk)
-                p = _attn_params(dtype, b, h, self.decay_factor, device)
+                p = _attn_params(dtype, b, h, self.decay_factor, device, odt)
                 rc = N.attn_accumulate(p, table, torch.cuda.current_stream(device).cuda_stream)
                 N.check(rc, "kvc_attn_accumulate")
                 for (li, _, _, _), acc in zip(jobs, accs):
@@ -154,9 +164,24 @@ class H2OAttentionManager:
 
 
 def run_heavy_hitters(mgr, rows, out_ptr, out_stride, stream):
-    """kvc_heavy_hitters over `rows` [(acc, m0, m, k)] (one dtype / batch / heads / device):
-    row i * B + b of the int32 array at out_ptr (row stride out_stride) receives the k ascending
-    indices."""
+    """kvc_heavy_hitters over `rows` [(acc, m0, m, k)]: row i * B + b of the int32 array at
+    out_ptr (row stride out_stride) receives the k ascending indices.  One launch when every
+    accumulation shares dtype, batch, heads and device; otherwise one per run of such rows (a
+    layer whose accumulation was promoted to float32, h2o_attention.py:129-151)."""
+    B = rows[0][0].shape[0]
+    runs, start = [], 0
+    for i in range(1, len(rows) + 1):
+        a, b = rows[start][0], rows[i][0] if i < len(rows) else None
+        if b is None or b.dtype != a.dtype or b.shape[:2] != a.shape[:2] or b.device != a.device:
+            runs.append((start, i))
+            start = i
+    for s0, s1 in runs:
+        if rows[s0][0].shape[0] != B:
+            raise RuntimeError("heavy hitters of layers with different batch sizes in one call")
+        _run_hh(mgr, rows[s0:s1], out_ptr + s0 * B * out_stride * 4, out_stride, stream)
+
+
+def _run_hh(mgr, rows, out_ptr, out_stride, stream):
     acc0 = rows[0][0]
     _check_gpu(acc0, "accumulated attention")
     B, H = acc0.shape[:2]
@@ -164,9 +189,6 @@ def run_heavy_hitters(mgr, rows, out_ptr, out_stride, stream):
     table = np.zeros(len(rows), dtype=N.HH_LAYER_DTYPE)
     keep = []
     for i, (acc, m0, m, k) in enumerate(rows):
-        if acc.dtype != acc0.dtype or acc.shape[:2] != (B, H) or acc.device != acc0.device:
-            raise NotImplementedError("heavy hitters of layers with different dtype / batch / "
-                                      "heads / device in one call")
         acc = acc.contiguous()
         keep.append(acc)
         table[i] = (acc.data_ptr(), acc.shape[-1], m0, m, k,
@@ -376,7 +398,7 @@ def _plan_step(kvl, attns, accs, mgr, start_size, heavy_hitter_size, recent_size
         if acc is not None and acc.size(-1) <= key_len:
             if acc.dtype != attn.dtype or acc.device != attn.device or \
                     acc.shape[:2] != attn.shape[:2]:
-                return None  # the Python path raises
+                return None  # mixed dtypes (promotion) / other devices: the Python path
             old_len = acc.size(-1)
         a_layers.append(li)
         a_rows.append((0, attn.stride()[:3], 0, 0, q, key_len, old_len,

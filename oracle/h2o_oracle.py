@@ -239,11 +239,16 @@ class H2OManager:
             imp = to_f32(attn_importance(attn, self.threads, self.capability))
             old = self.acc.get(li)
             base = np.zeros((B, H, k), np.float32)
+            out_dtype = attn.dtype
             if old is not None and old.shape[-1] <= k:
                 L = old.shape[-1]
-                dec = to_f32(old) * np.float32(self.decay_factor)  # (:136, :146)
-                base[:, :, :L] = to_f32(from_f32(dec, attn.dtype))
-            self.acc[li] = from_f32(base + imp, attn.dtype)      # (:149-151)
+                dec = to_f32(old) * np.float32(self.decay_factor)  # (:136, :146), in old's dtype
+                base[:, :, :L] = to_f32(from_f32(dec, old.dtype))
+                # torch.cat / + type promotion (:129-151): two different float dtypes of
+                # {bf16, fp16, fp32} promote to fp32 (exact widening of both operands)
+                if old.dtype != attn.dtype:
+                    out_dtype = np.float32
+            self.acc[li] = from_f32(base + imp, out_dtype)       # (:149-151)
             self.current_seq_len = k
 
     def get_heavy_hitter_indices(self, li, seq_len):

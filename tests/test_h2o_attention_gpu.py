@@ -269,3 +269,46 @@ def test_kv_batch_above_attention_batch_broadcasts_indices(dt):
         want = torch.cat([ref[:, :, :start], mid[:, :, idx], ref[:, :, -recent:]], dim=2)
         assert np.array_equal(to_np(x).view(np.uint8), to_np(want).view(np.uint8))
     assert [x.shape for x in out[1]] == [x.shape for x in out[0]]
+
+
+MIXED = json.load(open(os.path.join(HERE, "golden", "h2o_attention_mixed.json")))
+
+
+@pytest.mark.parametrize("si", [0, 1, 2])
+def test_engine_replays_reference_mixed_dtype_goldens(si):
+    """The carried accumulation and a new step's attention differ in dtype: the engine promotes as
+    the reference's `acc * decay`, torch.cat and `+` do (h2o_attention.py:129-151) -- float32
+    accumulations, heavy hitters and compressed K/V identical to the unmodified reference's
+    (tests/golden/gen_h2o_mixed_dtypes.py).  (A promoting step is never replayed natively: its
+    scan_h2o signature carries the accumulations' dtypes and _plan_step declines it.)"""
+    from gen_h2o_mixed_dtypes import att_seed as m_att, kv_seed as m_kv
+    from kvcompress.methods.h2o_attention import H2OAttentionManager, h2o_attention_compress
+    sc = MIXED["scenarios"][si]
+    H, D, L, kdt = MIXED["H"], MIXED["D"], MIXED["layers"], MIXED["kv_dtype"]
+    name = {torch.float32: "fp32", torch.bfloat16: "bf16", torch.float16: "fp16"}
+    mgr = H2OAttentionManager(decay_factor=sc["decay"], num_layers=L, num_heads=H, **sc["kw"])
+    mgr.reduction_threads = MIXED["threads"]
+    for st, step in enumerate(sc["steps"]):
+        k = step["k"] if step["op"] == "update" else step["S"]
+        atts = tuple(to_dev(h2o_inputs.attention(m_att(si, st, li), H, step["q"], k, step["dt"]))
+                     if step["att"][li] else None for li in range(L))
+        rec = MIXED["results"][sc["name"]][st]
+        if step["op"] == "update":
+            mgr.update_attention_scores(atts, skip_layers=step["skip"])
+            S = k
+        else:
+            S = step["S"]
+            kv = [(to_dev(prng.gen_keys(m_kv(si, st, li), (1, H, S, D), kdt)),
+                   to_dev(prng.gen_values(m_kv(si, st, li), (1, H, S, D), kdt)))
+                  for li in range(L)]
+            out = h2o_attention_compress(list(kv), attention_scores=atts, h2o_manager=mgr,
+                                         skip_layers=step["skip"], **sc["kw"])
+            for li in range(L):
+                assert out[li][0].shape[2] == rec["n_out"][li], (st, li)
+                assert sha(to_np(out[li][0])) == rec["k"][li], ("K", st, li)
+                assert sha(to_np(out[li][1])) == rec["v"][li], ("V", st, li)
+        for li in range(L):
+            acc = mgr.accumulated_attention.get(li)
+            assert (None if acc is None else name[acc.dtype]) == rec["acc_dtype"][li], (st, li)
+            assert (None if acc is None else sha(to_np(acc))) == rec["acc"][li], ("acc", st, li)
+            assert mgr.get_heavy_hitter_indices(li, S).cpu().tolist() == rec["idx"][li], (st, li)

@@ -178,3 +178,59 @@ def test_goldens_are_tie_heavy():
             return []
         replay(gold, si, "bf16", mgr, update_only, check)
     assert total >= 10 and tied >= total // 2, (tied, total)
+
+
+def mixed_golden():
+    with open(os.path.join(GOLD, "h2o_attention_mixed.json")) as f:
+        return json.load(f)
+
+
+def replay_mixed(gold, si, mgr, compress, check):
+    """One scenario of h2o_attention_mixed.json: each step's attention in its own dtype, K/V in
+    gold["kv_dtype"] (tests/golden/gen_h2o_mixed_dtypes.py)."""
+    from gen_h2o_mixed_dtypes import att_seed as m_att_seed, kv_seed as m_kv_seed
+    sc = gold["scenarios"][si]
+    H, D, L, kdt = gold["H"], gold["D"], gold["layers"], gold["kv_dtype"]
+    for st, step in enumerate(sc["steps"]):
+        k = step["k"] if step["op"] == "update" else step["S"]
+        atts = tuple(h2o_inputs.attention(m_att_seed(si, st, li), H, step["q"], k, step["dt"])
+                     if step["att"][li] else None for li in range(L))
+        out = None
+        if step["op"] == "update":
+            mgr.update_attention_scores(atts, skip_layers=step["skip"])
+            S = k
+        else:
+            S = step["S"]
+            kv = [(prng.gen_keys(m_kv_seed(si, st, li), (1, H, S, D), kdt),
+                   prng.gen_values(m_kv_seed(si, st, li), (1, H, S, D), kdt)) for li in range(L)]
+            out = compress(kv, atts, mgr, step["skip"], sc["kw"])
+        check(st, gold["results"][sc["name"]][st], S, out)
+
+
+NP_DTNAME = {np.dtype(np.float32): "fp32", np.dtype(np.uint16): "bf16",
+             np.dtype(np.float16): "fp16"}
+
+
+@pytest.mark.parametrize("si", [0, 1, 2])
+def test_oracle_replays_mixed_dtype_goldens(si):
+    """The carried accumulation and a new step's attention in different dtypes: the reference
+    promotes to fp32 through the decay, torch.cat and + (h2o_attention.py:129-151); a reset
+    starts over in the attention's dtype."""
+    gold = mixed_golden()
+    sc = gold["scenarios"][si]
+    mgr = HO.H2OManager(decay_factor=sc["decay"], threads=gold["threads"],
+                        capability=gold["capability"], **sc["kw"])
+
+    def compress(kv, atts, m, skip, kw):
+        return HO.h2o_attention_compress(kv, attention_scores=atts, h2o_manager=m,
+                                         skip_layers=skip, **kw)
+
+    def check(st, rec, S, out):
+        for li in range(gold["layers"]):
+            acc = mgr.acc.get(li)
+            assert (None if acc is None else NP_DTNAME[acc.dtype]) == rec["acc_dtype"][li]
+            assert (None if acc is None else sha(acc)) == rec["acc"][li], (st, li)
+            assert mgr.get_heavy_hitter_indices(li, S).tolist() == rec["idx"][li], (st, li)
+            if out is not None:
+                assert sha(out[li][0]) == rec["k"][li] and sha(out[li][1]) == rec["v"][li], (st, li)
+    replay_mixed(gold, si, mgr, compress, check)
