@@ -1922,11 +1922,23 @@ __global__ void __launch_bounds__(kSelThreads)
 // ---------------------------------------------------------------------------------------------
 // GATHER
 // ---------------------------------------------------------------------------------------------
+// Output rows a GATHER launch copies (KVC_FLAG_GATHER_FIXED / _SELECTED): all, the sink and
+// tail rows, or the selected rows -- as a count of "virtual" rows and the map to output rows.
+enum { PART_ALL = 0, PART_FIXED = 1, PART_SELECTED = 2 };
+__host__ __device__ __forceinline__ int part_rows(const kvc_layer_t& y, int part) {
+  return part == PART_FIXED ? y.sink_len + y.tail_len
+                            : part == PART_SELECTED ? y.n_select : y.sink_len + y.n_select +
+                                                                       y.tail_len;
+}
+__device__ __forceinline__ int part_row(int v, int sink, int nsel, int part) {
+  return part == PART_FIXED ? (v < sink ? v : v + nsel) : part == PART_SELECTED ? v + sink : v;
+}
+
 template <int DT, int NC, bool NTS>
 __global__ void __launch_bounds__(kGatherThreads)
     gather_kernel(const LayerChunk T, int H, int BH,
                   const int32_t* __restrict__ gidx, int64_t idx_stride, int shared,
-                  uint32_t* status) {
+                  uint32_t* status, int part) {
   const kvc_layer_t* L = T.l;
   // grid = (rows, output-token blocks); one block copies kGatherTokens output rows of K and V
   constexpr int ESZ = DTypeTraits<DT>::esz;
@@ -1935,9 +1947,10 @@ __global__ void __launch_bounds__(kGatherThreads)
   const kvc_layer_t* ly = L + grow / BH;
   const int r = grow - (grow / BH) * BH;
   const int n_out = ly->n_out;
+  const int nv = part_rows(*ly, part);  // rows this launch copies
   const int t0 = blockIdx.y * kGatherTokens;
-  if (t0 >= n_out) return;
-  const int nu = min(kGatherTokens, n_out - t0) * NC;
+  if (t0 >= nv) return;
+  const int nu = min(kGatherTokens, nv - t0) * NC;
   const int b = r / H, h = r - (r / H) * H;
   const int sink = ly->sink_len, nsel = ly->n_select;
   const char* kb = static_cast<const char*>(ly->k) +
@@ -1947,17 +1960,20 @@ __global__ void __launch_bounds__(kGatherThreads)
   const int64_t kss = ly->k_stride[2] * ESZ, vss = ly->v_stride[2] * ESZ;
   // index row of (layer, b, h); KVC_FLAG_SHARED_INDEX: (layer, b)'s row serves every head
   const int32_t* irow = gidx + (int64_t)((ly->row0 + r) / (shared ? H : 1)) * idx_stride;
-  const int64_t obase = ((int64_t)r * n_out + t0) * NC * 16;
+  const int64_t obase = (int64_t)r * n_out * NC * 16;
   char* ko = static_cast<char*>(ly->k_out) + obase;
   char* vo = static_cast<char*>(ly->v_out) + obase;
   uint4 xk[ITERS], xv[ITERS];
   bool gat[ITERS];
+  int64_t oofs[ITERS];
 #pragma unroll
   for (int i = 0; i < ITERS; ++i) {
     const int u = threadIdx.x + i * kGatherThreads;
     gat[i] = false;
+    oofs[i] = 0;
     if (u < nu) {
-      const int t = t0 + u / NC, c = u - (u / NC) * NC;
+      const int t = part_row(t0 + u / NC, sink, nsel, part), c = u - (u / NC) * NC;
+      oofs[i] = ((int64_t)t * NC + c) * 16;
       int src;
       if (t < sink) {
         src = t;
@@ -1987,12 +2003,12 @@ __global__ void __launch_bounds__(kGatherThreads)
       if constexpr (NTS) {
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         __builtin_nontemporal_store(u32x4{a.x, a.y, a.z, a.w},
-                                    reinterpret_cast<u32x4*>(ko + (int64_t)u * 16));
+                                    reinterpret_cast<u32x4*>(ko + oofs[i]));
         __builtin_nontemporal_store(u32x4{bq.x, bq.y, bq.z, bq.w},
-                                    reinterpret_cast<u32x4*>(vo + (int64_t)u * 16));
+                                    reinterpret_cast<u32x4*>(vo + oofs[i]));
       } else {
-        *reinterpret_cast<uint4*>(ko + (int64_t)u * 16) = a;
-        *reinterpret_cast<uint4*>(vo + (int64_t)u * 16) = bq;
+        *reinterpret_cast<uint4*>(ko + oofs[i]) = a;
+        *reinterpret_cast<uint4*>(vo + oofs[i]) = bq;
       }
     }
   }
@@ -2320,8 +2336,11 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
   if (p->batch < 1 || p->heads < 1 || p->head_dim < 1) return KVC_E_ARG;
   if (p->order != KVC_ASC && p->order != KVC_DESC) return KVC_E_ARG;
   if (p->algo != KVC_ALGO_SORT && p->algo != KVC_ALGO_TOPK) return KVC_E_ARG;
-  if ((p->flags & ~(KVC_FLAG_SPLIT_SELECT_GATHER | KVC_FLAG_SHARED_INDEX)) || p->reserved != 0)
+  if ((p->flags & ~(KVC_FLAG_SPLIT_SELECT_GATHER | KVC_FLAG_SHARED_INDEX | KVC_FLAG_GATHER_FIXED |
+                    KVC_FLAG_GATHER_SELECTED)) || p->reserved != 0)
     return KVC_E_ARG;  // unknown flag bits / reserved field: refuse rather than ignore
+  if ((p->flags & KVC_FLAG_GATHER_FIXED) && (p->flags & KVC_FLAG_GATHER_SELECTED))
+    return KVC_E_ARG;
   if ((p->flags & KVC_FLAG_SHARED_INDEX) && !p->external_index) return KVC_E_ARG;
   const int es = esize(p->dtype);
   const int rowb = p->head_dim * es;
@@ -2445,11 +2464,11 @@ static int launch_score(const LayerChunk& T, int nl, int H, int64_t tile_base,
 // `work` = max n_out over the chunk's layers; grid = (rows, token blocks)
 template <int DT, int NC>
 static int launch_gather(const LayerChunk& T, int nl, int H, int BH, const int32_t* idx,
-                         int64_t istride, int shared, uint32_t* status, int64_t work,
+                         int64_t istride, int shared, uint32_t* status, int64_t work, int part,
                          hipStream_t s) {
   const dim3 grid((unsigned)(nl * BH), (unsigned)((work + kGatherTokens - 1) / kGatherTokens));
   return launch_k(gather_kernel<DT, NC, true>, grid, dim3(kGatherThreads), 0, s, T, H, BH, idx,
-                  istride, shared, status);
+                  istride, shared, status, part);
 }
 
 // SELECT over the rows of a chunk (BH rows per layer, workspace row ly->row0 + blockIdx % BH):
@@ -2504,12 +2523,17 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
   memcpy(T.l, layers + c0, (size_t)cn * sizeof(kvc_layer_t));
   const int64_t tile_base = layers[c0].tile0;
   const int64_t tile_end = c0 + cn < nl ? (int64_t)layers[c0 + cn].tile0 : info.score_tiles;
+  const int part = (p->flags & KVC_FLAG_GATHER_FIXED)      ? PART_FIXED
+                   : (p->flags & KVC_FLAG_GATHER_SELECTED) ? PART_SELECTED
+                                                           : PART_ALL;
   bool sel = false, long_zone = false;
-  int64_t max_out = 0;
+  int64_t max_out = 0, max_part = 0;
   for (int l = c0; l < c0 + cn; ++l) {
     sel |= layers[l].n_select > 0;
     long_zone |= layer_selects(layers[l]) && layers[l].zone_len > kZoneMax;
     max_out = layers[l].n_out > max_out ? layers[l].n_out : max_out;
+    const int64_t pr = part_rows(layers[l], part);
+    max_part = pr > max_part ? pr : max_part;
   }
   const bool ext = p->external_index != 0;
   uint32_t* status = p->device_status;
@@ -2520,7 +2544,8 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
   const int n_cap = (int)nstride;  // longest zone of the call, rounded to 64
   if ((p->phases & KVC_PHASE_SELECT) && sel && !ext) {
     const bool fuse_sg = (p->phases & KVC_PHASE_GATHER) && max_out > 0 && !stamps &&
-                         !long_zone && !(p->flags & KVC_FLAG_SPLIT_SELECT_GATHER);
+                         !long_zone && part == PART_ALL &&
+                         !(p->flags & KVC_FLAG_SPLIT_SELECT_GATHER);
     if (fuse_sg) {  // this chunk's gather happens inside the select kernel
       const dim3 rows_grid((unsigned)(cn * BH));
       const int ks = (int)sizeof(KeyT);
@@ -2540,9 +2565,10 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
                            long_zone, scratch, st, status, s);
   }
   if (rc != KVC_OK) return rc;
-  if ((p->phases & KVC_PHASE_GATHER) && max_out > 0)
+  if ((p->phases & KVC_PHASE_GATHER) && max_part > 0)
     rc = launch_gather<DT, NC>(T, cn, H, BH, idx, istride,
-                               (p->flags & KVC_FLAG_SHARED_INDEX) ? 1 : 0, status, max_out, s);
+                               (p->flags & KVC_FLAG_SHARED_INDEX) ? 1 : 0, status, max_part, part,
+                               s);
   return rc;
 }
 

@@ -12,11 +12,13 @@
 //            caching-allocator block, contiguous [B,H,n_out,D] views), enqueues kvc_launch on the
 //            caller's stream and builds the result list (same objects, slices, outputs).
 // No arithmetic happens here; the kernels and the ABI are libkvc.so's (include/kvc.h).
+#include <hip/hip_runtime_api.h>
 #include <pybind11/numpy.h>
 #include <pybind11/stl.h>
 #include <torch/extension.h>
 
 #include <cstring>
+#include <map>
 #include <vector>
 
 #include "kvc.h"
@@ -91,21 +93,30 @@ py::object scan(py::list kv) {
   return std::move(sig);
 }
 
-// Outputs, table pointers, kvc_launch and the result list of a recorded call (run / run_h2o).
-py::list launch_and_list(PyObject* kv, const std::vector<at::Tensor>& ks,
-                         const std::vector<at::Tensor>& vs,
-                         const py::detail::unchecked_reference<int64_t, 2>& act, int64_t table_addr,
-                         int64_t n_jobs, const std::vector<int64_t>& n_outs, int64_t params_addr,
-                         int64_t ws, int64_t ws_bytes, int64_t stream) {
+// The outputs of a recorded call (one caching-allocator block: all K outputs, then all V
+// outputs) and its layer table with every pointer filled in.
+struct Prepared {
+  std::vector<at::Tensor> ko, vo;
+  std::vector<kvc_layer_t> table;
+};
+
+Prepared prepare(PyObject* kv, const std::vector<at::Tensor>& ks, const std::vector<at::Tensor>& vs,
+                 const py::detail::unchecked_reference<int64_t, 2>& act, int64_t table_addr,
+                 int64_t n_jobs, const std::vector<int64_t>& n_outs) {
   const Py_ssize_t L = PyList_GET_SIZE(kv);
-  std::vector<at::Tensor> ko(n_jobs), vo(n_jobs);
+  Prepared o;
+  o.ko.resize(n_jobs);
+  o.vo.resize(n_jobs);
   if (n_jobs > 0) {
+    std::vector<at::Tensor>& ko = o.ko;
+    std::vector<at::Tensor>& vo = o.vo;
     const at::Tensor& k0 = ks[0];
     const int64_t B = k0.size(0), H = k0.size(1), D = k0.size(3);
     int64_t total = 0;
     for (int64_t j = 0; j < n_jobs; ++j) total += 2 * B * H * n_outs[j] * D;
     at::Tensor buf = at::empty({total}, k0.options());
-    std::vector<kvc_layer_t> table(n_jobs);
+    std::vector<kvc_layer_t>& table = o.table;
+    table.resize(n_jobs);
     std::memcpy(table.data(), reinterpret_cast<const void*>(table_addr),
                 sizeof(kvc_layer_t) * n_jobs);
     int64_t off = 0;
@@ -128,12 +139,27 @@ py::list launch_and_list(PyObject* kv, const std::vector<at::Tensor>& ks,
       table[j].k_out = ko[j].data_ptr();
       table[j].v_out = vo[j].data_ptr();
     }
-    const int rc = kvc_launch(reinterpret_cast<const kvc_params_t*>(params_addr), table.data(),
-                              (int)n_jobs, reinterpret_cast<void*>(ws), (size_t)ws_bytes,
-                              reinterpret_cast<kvc_stream_t>(stream));
-    if (rc != KVC_OK)
-      throw std::runtime_error(std::string("kvc_launch failed: ") + kvc_status_string(rc));
   }
+  return o;
+}
+
+void launch(const Prepared& o, int64_t params_addr, int64_t ws, int64_t ws_bytes,
+            int64_t stream) {
+  if (o.table.empty()) return;
+  const int rc = kvc_launch(reinterpret_cast<const kvc_params_t*>(params_addr), o.table.data(),
+                            (int)o.table.size(), reinterpret_cast<void*>(ws), (size_t)ws_bytes,
+                            reinterpret_cast<kvc_stream_t>(stream));
+  if (rc != KVC_OK)
+    throw std::runtime_error(std::string("kvc_launch failed: ") + kvc_status_string(rc));
+}
+
+// The result list of a recorded call: per layer the input itself, a dim-2 slice, or its outputs.
+py::list result_list(PyObject* kv, const std::vector<at::Tensor>& ks,
+                     const std::vector<at::Tensor>& vs,
+                     const py::detail::unchecked_reference<int64_t, 2>& act, const Prepared& o) {
+  const Py_ssize_t L = PyList_GET_SIZE(kv);
+  const std::vector<at::Tensor>& ko = o.ko;
+  const std::vector<at::Tensor>& vo = o.vo;
   py::list out(L);
   for (Py_ssize_t i = 0; i < L; ++i) {
     const int64_t a = act(i, 0);
@@ -174,8 +200,36 @@ py::list run(py::list kv, py::array_t<int64_t, py::array::c_style> actions, int6
     throw std::invalid_argument("kvc_host.run: recorded call does not match the layer list");
   std::vector<at::Tensor> ks, vs;
   unpack_layers(kv.ptr(), ks, vs);
-  return launch_and_list(kv.ptr(), ks, vs, act, table_addr, n_jobs, n_outs, params_addr, ws,
-                         ws_bytes, stream);
+  const Prepared o = prepare(kv.ptr(), ks, vs, act, table_addr, n_jobs, n_outs);
+  launch(o, params_addr, ws, ws_bytes, stream);
+  return result_list(kv.ptr(), ks, vs, act, o);
+}
+
+// Per device: a second stream and two events (no timing, no system fence) with which run_h2o
+// copies the selection-independent output rows beside the heavy-hitter selection.  Created on
+// first use, kept for the life of the process.
+struct SideStream {
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
+const SideStream& side_stream() {
+  static std::map<int, SideStream> per_device;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) throw std::runtime_error("kvc_host: hipGetDevice failed");
+  SideStream& s = per_device[dev];
+  if (!s.side) {
+    const unsigned ef = hipEventDisableTiming | hipEventDisableSystemFence;
+    if (hipStreamCreateWithFlags(&s.side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&s.fork, ef) != hipSuccess ||
+        hipEventCreateWithFlags(&s.join, ef) != hipSuccess)
+      throw std::runtime_error("kvc_host: side stream / event creation failed");
+  }
+  return s;
+}
+
+void check_hip(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("kvc_host: ") + what + " failed");
 }
 
 // ---- h2o_attention (reference kvcompress/methods/h2o_attention.py:84-363) ---------------------
@@ -239,17 +293,33 @@ py::object scan_h2o(py::list kv, py::object attns, py::list accs) {
 //   idx, idx_stride : the gather plan's index region, where kvc_heavy_hitters writes
 //   the rest : as run()
 // Returns (result list, [acc_new of each accumulate row]).
+//   fixed_params, sel_params : when non-zero, the gather runs as two launches (kvc_params with
+//              KVC_FLAG_GATHER_FIXED / _SELECTED): the sink and recent rows on a side stream,
+//              forked from `stream` before the accumulate and joined after the selected rows'
+//              launch, so they copy while the heavy hitters are selected
 py::tuple run_h2o(py::list kv, py::object attns, py::list accs, std::vector<int64_t> a_layers,
                   int64_t a_table, int64_t a_params, std::vector<int64_t> hh_rows,
                   int64_t hh_table, int64_t hh_ws, int64_t hh_ws_bytes, int64_t idx,
                   int64_t idx_stride, py::array_t<int64_t, py::array::c_style> actions,
                   int64_t table_addr, int64_t n_jobs, std::vector<int64_t> n_outs,
-                  int64_t params_addr, int64_t ws, int64_t ws_bytes, int64_t stream) {
+                  int64_t params_addr, int64_t ws, int64_t ws_bytes, int64_t stream,
+                  int64_t fixed_params, int64_t sel_params) {
   const Py_ssize_t L = PyList_GET_SIZE(kv.ptr());
   auto act = actions.unchecked<2>();
   if (act.shape(0) != L || act.shape(1) != 3 || (int64_t)n_outs.size() != n_jobs ||
-      a_layers.empty())
+      a_layers.empty() || (fixed_params == 0) != (sel_params == 0))
     throw std::invalid_argument("kvc_host.run_h2o: recorded call does not match the inputs");
+  std::vector<at::Tensor> ks, vs;
+  unpack_layers(kv.ptr(), ks, vs);
+  const Prepared o = prepare(kv.ptr(), ks, vs, act, table_addr, n_jobs, n_outs);
+  const hipStream_t main = reinterpret_cast<hipStream_t>(stream);
+  const SideStream* side = nullptr;
+  if (fixed_params && !o.table.empty()) {  // the sink / recent rows, beside everything below
+    side = &side_stream();
+    check_hip(hipEventRecord(side->fork, main), "hipEventRecord");
+    check_hip(hipStreamWaitEvent(side->side, side->fork, 0), "hipStreamWaitEvent");
+    launch(o, fixed_params, ws, ws_bytes, reinterpret_cast<int64_t>(side->side));
+  }
   PyObject* seq = PySequence_Fast(attns.ptr(), "attention_scores must be a sequence");
   if (!seq) throw py::error_already_set();
   py::object hold = py::reinterpret_steal<py::object>(seq);
@@ -302,11 +372,12 @@ py::tuple run_h2o(py::list kv, py::object attns, py::list accs, std::vector<int6
                          reinterpret_cast<kvc_stream_t>(stream));
   if (rc != KVC_OK)
     throw std::runtime_error(std::string("kvc_heavy_hitters failed: ") + kvc_status_string(rc));
-  std::vector<at::Tensor> ks, vs;
-  unpack_layers(kv.ptr(), ks, vs);
-  py::list out = launch_and_list(kv.ptr(), ks, vs, act, table_addr, n_jobs, n_outs, params_addr,
-                                 ws, ws_bytes, stream);
-  return py::make_tuple(out, acc_out);
+  launch(o, side ? sel_params : params_addr, ws, ws_bytes, stream);
+  if (side) {
+    check_hip(hipEventRecord(side->join, side->side), "hipEventRecord");
+    check_hip(hipStreamWaitEvent(main, side->join, 0), "hipStreamWaitEvent");
+  }
+  return py::make_tuple(result_list(kv.ptr(), ks, vs, act, o), acc_out);
 }
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {

@@ -80,6 +80,7 @@ class HipEvent:
             h.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p,
                                               ctypes.c_void_p]
             h.hipEventDestroy.argtypes = [ctypes.c_void_p]
+            h.hipStreamWaitEvent.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
             cls._hip = h
         return cls._hip
 
@@ -94,6 +95,12 @@ class HipEvent:
         rc = self._lib().hipEventRecord(self._ev, stream.cuda_stream)
         if rc != 0:
             raise RuntimeError(f"hipEventRecord failed ({rc})")
+
+    def wait(self, stream):
+        """Make `stream` wait for this event's last recorded point (hipStreamWaitEvent)."""
+        rc = self._lib().hipStreamWaitEvent(stream.cuda_stream, self._ev, 0)
+        if rc != 0:
+            raise RuntimeError(f"hipStreamWaitEvent failed ({rc})")
 
     def elapsed_time(self, end):
         import ctypes
@@ -487,11 +494,27 @@ def _build_table(device, dtype, B, H, D, js):
     return np.array(rows, dtype=N.LAYER_DTYPE), kos, vos, keep
 
 
-def execute_shared(jobs: List[Segments], out_list: list, fill):
+_side = {}
+
+
+def side_stream(device):
+    """(stream, fork event, join event) of `device` for copies that overlap the current
+    stream's work (created once; the events have no timing and no system fence)."""
+    e = _side.get(device)
+    if e is None:
+        with torch.cuda.device(device):
+            e = (torch.cuda.Stream(device), HipEvent(), HipEvent())
+        _side[device] = e
+    return e
+
+
+def execute_shared(jobs: List[Segments], out_list: list, fill, overlap=False):
     """External-index GATHER whose index row (layer, b) serves every head of the layer
     (KVC_FLAG_SHARED_INDEX: h2o_attention's heavy hitters, one index list per layer).  Per group,
     `fill(js, index_region_ptr, row_stride, stream)` writes row (i * B + b) of job i before the
-    copy kernel is enqueued on the same stream."""
+    copy kernel is enqueued on the same stream.  overlap=True: the sink and tail rows (which no
+    index decides) are copied on a side stream forked before `fill` and joined after the selected
+    rows' copy (KVC_FLAG_GATHER_FIXED / _SELECTED), so they move while `fill` selects."""
     if _recording is not None:
         _recording.append(None)
     groups = {}
@@ -507,8 +530,19 @@ def execute_shared(jobs: List[Segments], out_list: list, fill):
             N.check(rc, "kvc_plan")
             ws = torch.empty(max(int(info.workspace_bytes), 256), dtype=torch.uint8,
                              device=torch.device("cuda", device))
+            side = side_stream(device) if overlap and _timer is None else None
+            if side is not None:
+                pf = _params(dtype, B, H, D, N.KVC_ASC, N.KVC_ALGO_SORT, True, shared=True)
+                pf.flags |= N.FLAG_GATHER_FIXED
+                p.flags |= N.FLAG_GATHER_SELECTED
+                side[1].record(stream)
+                side[1].wait(side[0])
+                _launch(pf, table, ws, info, side[0], pf.phases)
             fill(js, ws.data_ptr() + int(info.index_offset), int(info.index_row_stride), stream)
             _launch(p, table, ws, info, stream, p.phases)
+            if side is not None:  # `stream` continues only after the side copy
+                side[2].record(side[0])
+                side[2].wait(stream)
             del keep
         for j, ko, vo in zip(js, kos, vos):
             out_list[j.layer_idx] = (ko, vo)

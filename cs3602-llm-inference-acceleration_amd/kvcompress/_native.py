@@ -18,7 +18,7 @@ KVC_ASC, KVC_DESC = 0, 1
 KVC_ALGO_SORT, KVC_ALGO_TOPK = 0, 1
 KVC_SCORE_NORM, KVC_SCORE_SNAPKV = 0, 1
 PHASE_SCORE, PHASE_SELECT, PHASE_GATHER, PHASE_ALL = 1, 2, 4, 7
-FLAG_SPLIT_SELECT_GATHER, FLAG_SHARED_INDEX = 1, 2
+FLAG_SPLIT_SELECT_GATHER, FLAG_SHARED_INDEX, FLAG_GATHER_FIXED, FLAG_GATHER_SELECTED = 1, 2, 4, 8
 DEV_SELECT_BOUNDS, DEV_INDEX_RANGE = 1, 2  # enum kvc_device_status bits
 
 

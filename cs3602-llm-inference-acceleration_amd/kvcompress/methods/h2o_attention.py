@@ -271,6 +271,10 @@ def h2o_attention_compress(past_key_values, attention_scores: Optional[Tuple] = 
     return past_key_values
 
 
+# heavy-hitter middles at least this long copy their fixed rows beside the selection
+OVERLAP_MIN_ZONE = 4096
+
+
 def _compact_shared(mgr, jobs, n_hh, out_list):
     """One shared-index gather for the manager path: the index rows of the first n_hh jobs come
     from kvc_heavy_hitters (written in place when every row fits), the rest from host indices.
@@ -305,7 +309,10 @@ def _compact_shared(mgr, jobs, n_hh, out_list):
             for i, x in host:
                 if x is not None:
                     reg[i * B:(i + 1) * B, :x.numel()] = x.to(torch.int32)
-    E.execute_shared([s for s, _ in jobs], out_list, fill)
+    # long middles: the heavy-hitter selection takes a while, so the sink / recent rows copy
+    # beside it on a side stream
+    overlap = any(s.zone_len >= OVERLAP_MIN_ZONE for s, _ in jobs[:n_hh])
+    E.execute_shared([s for s, _ in jobs], out_list, fill, overlap=overlap)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -320,7 +327,8 @@ _NO_PLAN = object()  # step_memo entry of a shape that stays on the Python path
 
 class _StepPlan:
     __slots__ = ("a_layers", "a_table", "a_params", "hh_rows", "hh_table", "hh_ws", "idx",
-                 "idx_stride", "actions", "table", "n_outs", "params", "ws", "info", "seq_len")
+                 "idx_stride", "actions", "table", "n_outs", "params", "ws", "info", "seq_len",
+                 "p_fixed", "p_sel")
 
 
 def _replay_step(kvl, attention_scores, mgr, start_size, heavy_hitter_size, recent_size,
@@ -366,7 +374,8 @@ def _replay_step(kvl, attention_scores, mgr, start_size, heavy_hitter_size, rece
             plan.hh_ws.data_ptr(), int(plan.hh_ws.numel()), plan.idx, plan.idx_stride,
             plan.actions, plan.table.ctypes.data, len(plan.table), plan.n_outs,
             E.ctypes_addr(plan.params), plan.ws.data_ptr(), int(plan.info.workspace_bytes),
-            key[-1])
+            key[-1], E.ctypes_addr(plan.p_fixed) if plan.p_fixed is not None else 0,
+            E.ctypes_addr(plan.p_sel) if plan.p_sel is not None else 0)
     for li, a in zip(plan.a_layers, acc):
         mgr.accumulated_attention[li] = a
     mgr.current_seq_len = plan.seq_len
@@ -467,6 +476,12 @@ def _plan_step(kvl, attns, accs, mgr, start_size, heavy_hitter_size, recent_size
     for name in ("k", "v", "k_out", "v_out"):
         table[name] = 0
     plan.table, plan.params, plan.info = table, p, info
+    plan.p_fixed = plan.p_sel = None
+    if max(r[3] for r in hh) >= OVERLAP_MIN_ZONE:  # as _compact_shared: fixed rows beside
+        plan.p_fixed = E._params(keys.dtype, B, H, D, N.KVC_ASC, N.KVC_ALGO_SORT, True, shared=True)
+        plan.p_fixed.flags |= N.FLAG_GATHER_FIXED
+        plan.p_sel = E._params(keys.dtype, B, H, D, N.KVC_ASC, N.KVC_ALGO_SORT, True, shared=True)
+        plan.p_sel.flags |= N.FLAG_GATHER_SELECTED
     plan.n_outs = [int(x) for x in arr[:, 4] + arr[:, 3] + arr[:, 6]]
     plan.ws = torch.empty(max(int(info.workspace_bytes), 256), dtype=torch.uint8,
                           device=keys.device)

@@ -71,9 +71,16 @@ enum kvc_phase {
 };
 enum kvc_flag {
   KVC_FLAG_SPLIT_SELECT_GATHER = 1, /* SELECT writes the index region, then a GATHER kernel    */
-  KVC_FLAG_SHARED_INDEX = 2         /* external_index: index row (layer*batch + b) serves every
+  KVC_FLAG_SHARED_INDEX = 2,        /* external_index: index row (layer*batch + b) serves every
                                        head of (layer, b) -- h2o_attention's heavy hitters, one
                                        index list per layer (h2o_attention.py:326-333)        */
+  KVC_FLAG_GATHER_FIXED = 4,        /* GATHER copies only the sink and tail rows of each output
+                                       (the rows no selection decides), layout unchanged      */
+  KVC_FLAG_GATHER_SELECTED = 8      /* GATHER copies only the selected rows.  With the previous
+                                       flag: one call's copy in two launches, e.g. the fixed rows
+                                       on a second stream while the selection runs.  At most one
+                                       of the two; either implies SELECT and GATHER as two
+                                       kernels (as KVC_FLAG_SPLIT_SELECT_GATHER)               */
 };
 /* Bits the kernels OR into *params.device_status (when not NULL).  The word is sticky: the
  * library never clears it; the caller zeroes it and reads it after the stream has drained. */

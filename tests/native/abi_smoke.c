@@ -80,7 +80,7 @@ static int plan_checks(void) {
   CHECK(kvc_plan(&p, &l, 1, &info) == KVC_E_ARG, "n_select > zone rejected");
   l.n_select = 512;
   CHECK(kvc_launch(&p, &l, 1, NULL, 0, NULL) == KVC_E_WORKSPACE, "missing workspace rejected");
-  p.flags = 4;
+  p.flags = 16;
   CHECK(kvc_plan(&p, &l, 1, &info) == KVC_E_ARG, "unknown flag bit rejected");
   p.flags = 0;
   p.reserved = 1;

@@ -181,8 +181,13 @@ def test_plan_rejects_unknown_flags():
     must not be silently dropped by this library); SHARED_INDEX needs external indices."""
     table = np.array([_layer(100, 0, 100, 10)], dtype=N.LAYER_DTYPE)
     assert N.plan(_params(flags=N.FLAG_SPLIT_SELECT_GATHER), table.copy())[0] == 0
-    assert N.plan(_params(flags=4), table.copy())[0] == -1
+    assert N.plan(_params(flags=16), table.copy())[0] == -1
     assert N.plan(_params(flags=1 << 30), table.copy())[0] == -1
+    # the gather-part flags: one at a time
+    assert N.plan(_params(flags=N.FLAG_GATHER_FIXED), table.copy())[0] == 0
+    assert N.plan(_params(flags=N.FLAG_GATHER_SELECTED), table.copy())[0] == 0
+    assert N.plan(_params(flags=N.FLAG_GATHER_FIXED | N.FLAG_GATHER_SELECTED),
+                  table.copy())[0] == -1
     assert N.plan(_params(reserved=1), table.copy())[0] == -1
     assert N.plan(_params(flags=N.FLAG_SHARED_INDEX), table.copy())[0] == -1
     assert N.plan(_params(flags=N.FLAG_SHARED_INDEX, external_index=1,

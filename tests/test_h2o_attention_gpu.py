@@ -312,3 +312,41 @@ def test_engine_replays_reference_mixed_dtype_goldens(si):
             assert (None if acc is None else name[acc.dtype]) == rec["acc_dtype"][li], (st, li)
             assert (None if acc is None else sha(to_np(acc))) == rec["acc"][li], ("acc", st, li)
             assert mgr.get_heavy_hitter_indices(li, S).cpu().tolist() == rec["idx"][li], (st, li)
+
+
+def test_fixed_rows_copied_beside_the_selection_match():
+    """Middles >= OVERLAP_MIN_ZONE: the sink / recent rows are copied on a side stream while the
+    heavy hitters are selected (KVC_FLAG_GATHER_FIXED / _SELECTED), in the Python path and in the
+    native step replay; every output equals the single-launch copy's."""
+    from kvcompress.methods import h2o_attention as HA
+    rng = np.random.default_rng(11)
+    L, H, S, D = 3, 8, 6000, 64
+    kw = dict(start_size=4, heavy_hitter_size=64, recent_size=444, skip_layers=[])
+    kv = [(to_dev(prng.gen_keys(40 + i, (1, H, S, D), "bf16")),
+           to_dev(prng.gen_values(40 + i, (1, H, S, D), "bf16"))) for i in range(L)]
+    att = tuple(_tie_attention(rng, (1, H, 1, S)).to(torch.bfloat16).to("cuda:0")
+                for _ in range(L))
+    mk = lambda: HA.H2OAttentionManager(start_size=4, heavy_hitter_size=64,  # noqa: E731
+                                        recent_size=444)
+    saved = HA.OVERLAP_MIN_ZONE
+    try:
+        HA.OVERLAP_MIN_ZONE = 1 << 30  # one launch
+        HA.replay_steps = False
+        ref = HA.h2o_attention_compress(list(kv), attention_scores=att, h2o_manager=mk(), **kw)
+        HA.OVERLAP_MIN_ZONE = saved
+        got = HA.h2o_attention_compress(list(kv), attention_scores=att, h2o_manager=mk(), **kw)
+        HA.replay_steps = True
+        HA.step_memo.clear()
+        r0 = HA.step_stats["replayed"]
+        mgr = mk()
+        for _ in range(4):  # the 3rd and 4th calls are native replays (fresh accumulations)
+            mgr.reset()
+            rep = HA.h2o_attention_compress(list(kv), attention_scores=att, h2o_manager=mgr, **kw)
+        assert HA.step_stats["replayed"] - r0 >= 2
+    finally:
+        HA.OVERLAP_MIN_ZONE = saved
+        HA.replay_steps = True
+    for outs in (got, rep):
+        for li in range(L):
+            for x, y in zip(outs[li], ref[li]):
+                assert np.array_equal(to_np(x).view(np.uint8), to_np(y).view(np.uint8)), li
