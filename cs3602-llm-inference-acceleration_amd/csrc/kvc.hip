@@ -721,35 +721,63 @@ __device__ __forceinline__ void wave_stable_sort(KeyT* key, uint16_t* idx, int l
 //     not increase with depth (heap order), so it stops at depth m = #{path nodes below `top`
 //     with !(key < value)}, and its moves undo the down phase below m.
 // Net effect: path depths 0..m-1 take their chosen child's entry, depth m takes the value, the
-// rest of the heap is unchanged.  Each lane derives its chosen child from its children's keys
-// (ds_bpermute), the path is a chase of <= 7 readlanes, and m is one ballot.
+// rest of the heap is unchanged; m is one ballot.
+// PACKED (16-bit keys and positions): slot j's entry is one word, key << 16 | index, so each
+// pop permutes one register instead of two (the children's keys and indices travel together).
+template <bool PACKED>
 struct RegHeap {
-  uint32_t hk;
-  uint32_t hi;
+  uint32_t hk;  // PACKED: key << 16 | index
+  uint32_t hi;  // !PACKED: index
+  __device__ __forceinline__ uint32_t key_of(uint32_t x) const { return PACKED ? x >> 16 : x; }
   __device__ __forceinline__ uint32_t k(int j) const {
-    return (uint32_t)__builtin_amdgcn_readlane((int)hk, j);
+    return key_of((uint32_t)__builtin_amdgcn_readlane((int)hk, j));
   }
+  __device__ __forceinline__ uint32_t i(int j) const {
+    const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)(PACKED ? hk : hi), j);
+    return PACKED ? x & 0xFFFFu : x;
+  }
+  __device__ __forceinline__ void set(uint32_t key, uint32_t ix) {
+    if constexpr (PACKED) hk = key << 16 | ix;
+    else hk = key, hi = ix;
+  }
+  // The path is found without a chase: every child lane learns from its sibling's key (a DPP
+  // wave shift, no LDS round trip) whether its parent chose it, one ballot collects those bits,
+  // and each lane walks its <= 6 ancestors in registers; each parent then pulls its chosen
+  // child's entry with one ds_bpermute issued as soon as the ballot is known.  (Round 3's
+  // readlane chase cost ~870 cycles per pop, tools/heap_probe.hip.)
   __device__ __forceinline__ void adjust(int top, int len, uint32_t vk, uint32_t vi) {
     const int lane = (int)(threadIdx.x & 63);
-    const int l = min(2 * lane + 1, 63), r = min(2 * lane + 2, 63);
-    const uint32_t kl = (uint32_t)__builtin_amdgcn_ds_bpermute(l * 4, (int)hk);
-    const uint32_t kr = (uint32_t)__builtin_amdgcn_ds_bpermute(r * 4, (int)hk);
-    const uint32_t il = (uint32_t)__builtin_amdgcn_ds_bpermute(l * 4, (int)hi);
-    const uint32_t ir = (uint32_t)__builtin_amdgcn_ds_bpermute(r * 4, (int)hi);
-    const bool two = lane < (len - 1) / 2;                       // both children in the heap
-    const bool lone = (len & 1) == 0 && lane == (len - 2) / 2;   // only the left one
-    const bool left = lone || (two && kr < kl);
-    const int ch = two || lone ? (left ? l : r) : -1;
-    const uint32_t ck = left ? kl : kr, ci = left ? il : ir;
-    int depth = -1;
-    for (int cur = top, d = 0; cur >= 0; ++d) {  // wave-uniform chase, <= log2(len) + 1 steps
-      depth = lane == cur ? d : depth;
-      cur = __builtin_amdgcn_readlane(ch, cur);
+    const uint32_t key = key_of(hk);
+    const uint32_t kn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key, 0x130, 0xF, 0xF, false);  // wave_shl:1: lane + 1
+    const uint32_t kp = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key, 0x138, 0xF, 0xF, false);  // wave_shr:1: lane - 1
+    const int p = (lane - 1) >> 1;                              // parent of this lane
+    const bool two = p < (len - 1) / 2;                         // the parent has both children
+    const bool lone = (len & 1) == 0 && p == (len - 2) / 2;     // only the left one
+    // std::__adjust_heap: the right child unless it is strictly smaller than the left
+    const bool cb = lane >= 1 && lane < len &&
+                    ((lane & 1) ? (lone || (two && kn < key)) : (two && !(key < kp)));
+    const uint64_t B = __builtin_amdgcn_ballot_w64(cb);
+    const int c1 = min(2 * lane + 1, 63);
+    const int ch = ((B >> c1) & 1ull) ? c1 : min(2 * lane + 2, 63);  // chosen child (path nodes)
+    const uint32_t ck = (uint32_t)__builtin_amdgcn_ds_bpermute(ch * 4, (int)hk);
+    uint32_t ci = 0;
+    if constexpr (!PACKED) ci = (uint32_t)__builtin_amdgcn_ds_bpermute(ch * 4, (int)hi);
+    // on the path from `top` iff every link from top down to this lane is a chosen one
+    int a = lane, d = 0;
+    bool ok = lane >= top;
+#pragma unroll
+    for (int st = 0; st < 6; ++st) {  // heaps of <= 64 slots: depth <= 6
+      const bool step = a > top;
+      ok = ok && (!step || ((B >> a) & 1ull));
+      a = step ? (a - 1) >> 1 : a;
+      d += step ? 1 : 0;
     }
-    const int m = __popcll(__builtin_amdgcn_ballot_w64(depth >= 1 && !(hk < vk)));
-    const bool up = depth >= 0 && depth < m, here = depth == m;
-    hk = up ? ck : here ? vk : hk;
-    hi = up ? ci : here ? vi : hi;
+    const bool onpath = ok && a == top;
+    const int m = __popcll(__builtin_amdgcn_ballot_w64(onpath && d >= 1 && !(key < vk)));
+    const bool up = onpath && d < m, here = onpath && d == m;
+    const uint32_t v = PACKED ? (vk << 16 | vi) : vk;
+    hk = up ? ck : here ? v : hk;
+    if constexpr (!PACKED) hi = up ? ci : here ? vi : hi;
   }
 };
 
@@ -757,31 +785,42 @@ template <typename K, typename I>
 __device__ __forceinline__ void wave_heap_select(K* key, I* idx, int middle, int len) {
   const int lane = threadIdx.x & 63;
   if (middle <= 64) {  // the heap in registers (RegHeap): make_heap, then the scan with its pops
-    RegHeap h;
-    h.hk = lane < middle ? (uint32_t)key[lane] : 0u;
-    h.hi = lane < middle ? (uint32_t)idx[lane] : 0u;
+    constexpr bool PK = sizeof(K) == 2 && sizeof(I) == 2;
+    RegHeap<PK> h;
+    h.set(lane < middle ? (uint32_t)key[lane] : 0u, lane < middle ? (uint32_t)idx[lane] : 0u);
     if (middle >= 2)
       for (int parent = (middle - 2) / 2; parent >= 0; --parent)
-        h.adjust(parent, middle, h.k(parent), (uint32_t)__builtin_amdgcn_readlane((int)h.hi, parent));
+        h.adjust(parent, middle, h.k(parent), h.i(parent));
     uint32_t top = h.k(0);
-    for (int base = middle; base < len; base += 64) {
-      const int i = base + lane;
-      const uint32_t ki = i < len ? (uint32_t)key[i] : 0xFFFFFFFFu;
-      const uint32_t ii = i < len ? (uint32_t)idx[i] : 0u;
-      uint64_t cand = __builtin_amdgcn_ballot_w64(i < len && ki < top);
-      while (cand) {
-        const int l = (int)__builtin_ctzll(cand);
-        // std::__pop_heap(first, middle, i): the old top goes to position i (never read again:
-        // only the heap's slots are the result), element i sifts in from the root
-        h.adjust(0, middle, (uint32_t)__builtin_amdgcn_readlane((int)ki, l),
-                 (uint32_t)__builtin_amdgcn_readlane((int)ii, l));
-        top = h.k(0);
-        cand &= ~((2ull << l) - 1ull) & __builtin_amdgcn_ballot_w64(ki < top);
+    // the scan, four rows of 64 candidates per LDS round trip (the loads do not depend on the
+    // heap; only the ballots and pops do)
+    constexpr int R = 4;
+    for (int base = middle; base < len; base += 64 * R) {
+      uint32_t kq[R], iq[R];
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        const int i = base + q * 64 + lane;
+        kq[q] = i < len ? (uint32_t)key[i] : 0xFFFFFFFFu;
+        iq[q] = i < len ? (uint32_t)idx[i] : 0u;
+      }
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        // lanes past len hold ~0, never below top; 16-bit keys are below 2^16
+        uint64_t cand = __builtin_amdgcn_ballot_w64(kq[q] < top);
+        while (cand) {
+          const int l = (int)__builtin_ctzll(cand);
+          // std::__pop_heap(first, middle, i): the old top goes to position i (never read again:
+          // only the heap's slots are the result), element i sifts in from the root
+          h.adjust(0, middle, (uint32_t)__builtin_amdgcn_readlane((int)kq[q], l),
+                   (uint32_t)__builtin_amdgcn_readlane((int)iq[q], l));
+          top = h.k(0);
+          cand &= ~((2ull << l) - 1ull) & __builtin_amdgcn_ballot_w64(kq[q] < top);
+        }
       }
     }
     if (lane < middle) {
-      key[lane] = (K)h.hk;
-      idx[lane] = (I)h.hi;
+      key[lane] = (K)h.key_of(h.hk);
+      idx[lane] = (I)(PK ? (h.hk & 0xFFFFu) : h.hi);
     }
     wave_sync();
     return;
@@ -1934,21 +1973,20 @@ __device__ __forceinline__ int part_row(int v, int sink, int nsel, int part) {
   return part == PART_FIXED ? (v < sink ? v : v + nsel) : part == PART_SELECTED ? v + sink : v;
 }
 
+// One block of the copy: kGatherTokens output rows of K and V of workspace row `grow`
+// (layer * BH + b * H + h), token block `by`.
 template <int DT, int NC, bool NTS>
-__global__ void __launch_bounds__(kGatherThreads)
-    gather_kernel(const LayerChunk T, int H, int BH,
-                  const int32_t* __restrict__ gidx, int64_t idx_stride, int shared,
-                  uint32_t* status, int part) {
-  const kvc_layer_t* L = T.l;
-  // grid = (rows, output-token blocks); one block copies kGatherTokens output rows of K and V
+__device__ __forceinline__ void gather_block(const kvc_layer_t* __restrict__ L, int H, int BH,
+                                             const int32_t* __restrict__ gidx,
+                                             int64_t idx_stride, int shared, uint32_t* status,
+                                             int part, int grow, int by) {
   constexpr int ESZ = DTypeTraits<DT>::esz;
   constexpr int ITERS = (kGatherTokens * NC + kGatherThreads - 1) / kGatherThreads;
-  const int grow = blockIdx.x;
   const kvc_layer_t* ly = L + grow / BH;
   const int r = grow - (grow / BH) * BH;
   const int n_out = ly->n_out;
   const int nv = part_rows(*ly, part);  // rows this launch copies
-  const int t0 = blockIdx.y * kGatherTokens;
+  const int t0 = by * kGatherTokens;
   if (t0 >= nv) return;
   const int nu = min(kGatherTokens, nv - t0) * NC;
   const int b = r / H, h = r - (r / H) * H;
@@ -2012,6 +2050,25 @@ __global__ void __launch_bounds__(kGatherThreads)
       }
     }
   }
+}
+
+// grid = (rows, output-token blocks), one block each -- or, with loop_rows > 0, a capped 1-D grid
+// whose blocks stride over the rows * nby blocks (the fixed rows of h2o_attention copied beside
+// its heavy-hitter selection: a few resident workgroups per CU leave room for the selection's).
+template <int DT, int NC, bool NTS>
+__global__ void __launch_bounds__(kGatherThreads)
+    gather_kernel(const LayerChunk T, int H, int BH, const int32_t* __restrict__ gidx,
+                  int64_t idx_stride, int shared, uint32_t* status, int part, int loop_rows,
+                  int nby) {
+  if (loop_rows == 0) {
+    gather_block<DT, NC, NTS>(T.l, H, BH, gidx, idx_stride, shared, status, part, blockIdx.x,
+                              blockIdx.y);
+    return;
+  }
+  const int nvb = loop_rows * nby;
+  for (int vb = blockIdx.x; vb < nvb; vb += gridDim.x)
+    gather_block<DT, NC, NTS>(T.l, H, BH, gidx, idx_stride, shared, status, part, vb % loop_rows,
+                              vb / loop_rows);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2248,35 +2305,112 @@ constexpr int kColThreads = 256;
 // ODT: dtype of acc_old.  ODT != DT (the carried accumulation and the new attention differ in
 // dtype, every layer carried): base is rounded to ODT, and acc_new is fp32 -- torch's promotion
 // of two different float dtypes through torch.cat / + (:129-151) -- holding fp32(base) + fp32(imp).
+// V consecutive elements of dtype DT at element offset i of `base` as floats: one 16-B load when
+// the span is whole and 16-B aligned, else element by element (n valid, the rest 0).
+template <int DT, int V>
+__device__ __forceinline__ void load_vec(const char* base, int64_t i, int n, float (&x)[V]) {
+  constexpr int ESZ = DTypeTraits<DT>::esz;
+  constexpr int PER = 16 / ESZ;  // elements per 16-B load
+  const char* p = base + i * ESZ;
+  if (n == V && V % PER == 0 && ((uintptr_t)p & 15u) == 0) {
+#pragma unroll
+    for (int c = 0; c < V / PER; ++c) {
+      const uint4 w = reinterpret_cast<const uint4*>(p)[c];
+      const uint32_t u[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int e = 0; e < PER; ++e) {
+        if constexpr (DT == KVC_F32) x[c * PER + e] = bits_to_f32(u[e]);
+        else if constexpr (DT == KVC_BF16)
+          x[c * PER + e] = bf16_to_f32((u[e / 2] >> (16 * (e & 1))) & 0xFFFFu);
+        else x[c * PER + e] = f16_to_f32((u[e / 2] >> (16 * (e & 1))) & 0xFFFFu);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < V; ++e) x[e] = e < n ? load_dt<DT>(p, e) : 0.f;
+  }
+}
+
+// The first n of V floats stored as dtype DT at element offset i of `base` (rounded as
+// store_dt): 16-B stores when the span is whole and aligned.
+template <int DT, int V>
+__device__ __forceinline__ void store_vec(void* base, int64_t i, int n, const float (&x)[V]) {
+  constexpr int ESZ = DTypeTraits<DT>::esz;
+  char* p = static_cast<char*>(base) + i * ESZ;
+  constexpr int PER = 16 / ESZ;  // elements per 16-B store
+  if (n == V && V % PER == 0 && ((uintptr_t)p & 15u) == 0) {
+#pragma unroll
+    for (int c = 0; c < V / PER; ++c) {
+      uint32_t u[4];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        if constexpr (DT == KVC_F32) u[w] = f32_to_bits(x[c * PER + w]);
+        else u[w] = store_bits<DT>(x[c * PER + 2 * w]) | (store_bits<DT>(x[c * PER + 2 * w + 1]) << 16);
+      }
+      *reinterpret_cast<uint4*>(p + c * 16) = make_uint4(u[0], u[1], u[2], u[3]);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < V; ++e)
+      if (e < n) store_dt<DT>(base, i + e, x[e]);
+  }
+}
+
+// ODT: dtype of acc_old.  ODT != DT (the carried accumulation and the new attention differ in
+// dtype, every layer carried): base is rounded to ODT, and acc_new is fp32 -- torch's promotion
+// of two different float dtypes through torch.cat / + (:129-151) -- holding fp32(base) + fp32(imp).
+// One thread per kAccCols consecutive key columns (16-B loads and stores where aligned): with one
+// column per thread a 32-layer decode step's [32, 16 384] rows took 65 536 workgroups and the
+// launch ~130 us, bound by workgroup turnover, not bytes.
+constexpr int kAccCols = 8;
 template <int DT, int ODT>
 __global__ void __launch_bounds__(kColThreads)
     attn_accum_kernel(const AttnChunk T, int H, int BH, float decay, int group, int vec_min) {
   constexpr int ESZ = DTypeTraits<DT>::esz;
   constexpr int NDT = ODT == DT ? DT : KVC_F32;  // acc_new's dtype
+  constexpr int V = kAccCols;
   const kvc_attn_layer_t* ly = T.l + blockIdx.x / BH;
   const int r = (int)(blockIdx.x % BH);
-  const int j = (int)blockIdx.y * kColThreads + (int)threadIdx.x;
+  const int j0 = ((int)blockIdx.y * kColThreads + (int)threadIdx.x) * V;
   const int k = ly->key_len;
-  if (j >= k) return;
+  if (j0 >= k) return;
+  const int n = min(V, k - j0);
   const int b = r / H, h = r - (r / H) * H;
   const char* a = static_cast<const char*>(ly->attn) +
-                  ((int64_t)b * ly->attn_stride[0] + (int64_t)h * ly->attn_stride[1] + j) * ESZ;
+                  ((int64_t)b * ly->attn_stride[0] + (int64_t)h * ly->attn_stride[1]) * ESZ;
   const int64_t qs = ly->attn_stride[2] * ESZ;
-  const auto ld = [&](int i) { return load_dt<DT>(a + (int64_t)i * qs, 0); };
   const int q = ly->q_len;
-  float s;
-  if (q == 1)
-    s = 0.f + ld(0);  // no reduction: the elementwise out = 0 + x
-  else if (col_ilp(j, k, ly->col_chunk, 128 / ESZ, group, vec_min))
-    s = 0.f + ilp4_sum(ld, q);  // the accumulating store adds to the zero-filled output
-  else
-    s = 0.f + cascade_sum(ld, q, 0, 1);
-  const float imp = round_dt<DT>(s);
-  float base = 0.f;
-  if (j < ly->old_len)
-    base = round_dt<ODT>(load_dt<ODT>(static_cast<const char*>(ly->acc_old),
-                                      (int)((int64_t)r * ly->old_len + j)) * decay);
-  store_dt<NDT>(ly->acc_new, (int64_t)r * k + j, base + imp);
+  float s[V];
+  if (q == 1) {  // no reduction: the elementwise out = 0 + x
+    load_vec<DT, V>(a, j0, n, s);
+#pragma unroll
+    for (int e = 0; e < V; ++e) s[e] = 0.f + s[e];
+  } else {
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const int j = j0 + e;
+      if (e >= n) {
+        s[e] = 0.f;
+        continue;
+      }
+      const auto ld = [&](int i) { return load_dt<DT>(a + (int64_t)i * qs, j); };
+      // the accumulating store adds to the zero-filled output
+      s[e] = col_ilp(j, k, ly->col_chunk, 128 / ESZ, group, vec_min) ? 0.f + ilp4_sum(ld, q)
+                                                                      : 0.f + cascade_sum(ld, q, 0, 1);
+    }
+  }
+  float base[V];
+  const int nold = min(n, ly->old_len - j0);  // carried columns of this thread (may be <= 0)
+  if (nold > 0)
+    load_vec<ODT, V>(static_cast<const char*>(ly->acc_old), (int64_t)r * ly->old_len + j0, nold,
+                     base);
+  float out[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    const float bse = e < nold ? round_dt<ODT>(base[e] * decay) : 0.f;
+    out[e] = bse + round_dt<DT>(s[e]);
+  }
+  store_vec<NDT, V>(ly->acc_new, (int64_t)r * k + j0, n, out);
 }
 
 // get_heavy_hitter_indices' head sum (h2o_attention.py:194-198) for every layer of the chunk:
@@ -2462,13 +2596,19 @@ static int launch_score(const LayerChunk& T, int nl, int H, int64_t tile_base,
 }
 
 // `work` = max n_out over the chunk's layers; grid = (rows, token blocks)
+// KVC_FLAG_GATHER_FIXED launches (copies meant to run beside a selection on another stream) use
+// at most this many workgroups: two of four waves per CU
+constexpr int kFixedGatherBlocks = 512;
 template <int DT, int NC>
 static int launch_gather(const LayerChunk& T, int nl, int H, int BH, const int32_t* idx,
                          int64_t istride, int shared, uint32_t* status, int64_t work, int part,
                          hipStream_t s) {
-  const dim3 grid((unsigned)(nl * BH), (unsigned)((work + kGatherTokens - 1) / kGatherTokens));
-  return launch_k(gather_kernel<DT, NC, true>, grid, dim3(kGatherThreads), 0, s, T, H, BH, idx,
-                  istride, shared, status, part);
+  const int rows = nl * BH, nby = (int)((work + kGatherTokens - 1) / kGatherTokens);
+  if (part == PART_FIXED && (int64_t)rows * nby > kFixedGatherBlocks)
+    return launch_k(gather_kernel<DT, NC, true>, dim3(kFixedGatherBlocks), dim3(kGatherThreads), 0,
+                    s, T, H, BH, idx, istride, shared, status, part, rows, nby);
+  return launch_k(gather_kernel<DT, NC, true>, dim3((unsigned)rows, (unsigned)nby),
+                  dim3(kGatherThreads), 0, s, T, H, BH, idx, istride, shared, status, part, 0, nby);
 }
 
 // SELECT over the rows of a chunk (BH rows per layer, workspace row ly->row0 + blockIdx % BH):
@@ -2638,7 +2778,8 @@ static int accumulate_impl(const kvc_attn_params_t* p, const kvc_attn_layer_t* l
         (p->flags && y.old_len == 0) || (uintptr_t)y.attn % es ||
         (uintptr_t)y.acc_new % nes || (uintptr_t)y.acc_old % oes)
       return KVC_E_ARG;
-    if ((y.key_len + kColThreads - 1) / kColThreads > 65535) return KVC_E_TOO_LONG;
+    if ((y.key_len + kColThreads * kAccCols - 1) / (kColThreads * kAccCols) > 65535)
+      return KVC_E_TOO_LONG;
   }
   const int H = p->heads, BH = p->batch * p->heads;
   const int group = 4 * (p->vec_bytes / 4), vec_min = p->vec_bytes / es;
@@ -2648,7 +2789,8 @@ static int accumulate_impl(const kvc_attn_params_t* p, const kvc_attn_layer_t* l
     memcpy(T.l, layers + c0, (size_t)cn * sizeof(kvc_attn_layer_t));
     int kmax = 0;
     for (int l = 0; l < cn; ++l) kmax = T.l[l].key_len > kmax ? T.l[l].key_len : kmax;
-    const dim3 grid((unsigned)(cn * BH), (unsigned)((kmax + kColThreads - 1) / kColThreads));
+    const int cols = kColThreads * kAccCols;
+    const dim3 grid((unsigned)(cn * BH), (unsigned)((kmax + cols - 1) / cols));
     rc = with_dtype(p->dtype, [&](auto dt) {
       return with_dtype(odt, [&](auto od) {
         return launch_k(attn_accum_kernel<decltype(dt)::value, decltype(od)::value>, grid,

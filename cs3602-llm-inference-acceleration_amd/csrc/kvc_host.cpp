@@ -295,8 +295,8 @@ py::object scan_h2o(py::list kv, py::object attns, py::list accs) {
 // Returns (result list, [acc_new of each accumulate row]).
 //   fixed_params, sel_params : when non-zero, the gather runs as two launches (kvc_params with
 //              KVC_FLAG_GATHER_FIXED / _SELECTED): the sink and recent rows on a side stream,
-//              forked from `stream` before the accumulate and joined after the selected rows'
-//              launch, so they copy while the heavy hitters are selected
+//              forked from `stream` after the accumulate (which they would slow down) and joined
+//              after the selected rows' launch, so they copy while the heavy hitters are selected
 py::tuple run_h2o(py::list kv, py::object attns, py::list accs, std::vector<int64_t> a_layers,
                   int64_t a_table, int64_t a_params, std::vector<int64_t> hh_rows,
                   int64_t hh_table, int64_t hh_ws, int64_t hh_ws_bytes, int64_t idx,
@@ -314,12 +314,6 @@ py::tuple run_h2o(py::list kv, py::object attns, py::list accs, std::vector<int6
   const Prepared o = prepare(kv.ptr(), ks, vs, act, table_addr, n_jobs, n_outs);
   const hipStream_t main = reinterpret_cast<hipStream_t>(stream);
   const SideStream* side = nullptr;
-  if (fixed_params && !o.table.empty()) {  // the sink / recent rows, beside everything below
-    side = &side_stream();
-    check_hip(hipEventRecord(side->fork, main), "hipEventRecord");
-    check_hip(hipStreamWaitEvent(side->side, side->fork, 0), "hipStreamWaitEvent");
-    launch(o, fixed_params, ws, ws_bytes, reinterpret_cast<int64_t>(side->side));
-  }
   PyObject* seq = PySequence_Fast(attns.ptr(), "attention_scores must be a sequence");
   if (!seq) throw py::error_already_set();
   py::object hold = py::reinterpret_steal<py::object>(seq);
@@ -358,6 +352,12 @@ py::tuple run_h2o(py::list kv, py::object attns, py::list accs, std::vector<int6
                                (int)na, reinterpret_cast<kvc_stream_t>(stream));
   if (rc != KVC_OK)
     throw std::runtime_error(std::string("kvc_attn_accumulate failed: ") + kvc_status_string(rc));
+  if (fixed_params && !o.table.empty()) {  // the sink / recent rows, beside the heavy hitters
+    side = &side_stream();
+    check_hip(hipEventRecord(side->fork, main), "hipEventRecord");
+    check_hip(hipStreamWaitEvent(side->side, side->fork, 0), "hipStreamWaitEvent");
+    launch(o, fixed_params, ws, ws_bytes, reinterpret_cast<int64_t>(side->side));
+  }
   const size_t nh = hh_rows.size();
   std::vector<kvc_hh_layer_t> ht(nh);
   std::memcpy(ht.data(), reinterpret_cast<const void*>(hh_table), sizeof(kvc_hh_layer_t) * nh);

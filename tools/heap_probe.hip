@@ -1,0 +1,100 @@
+// heap_probe.hip -- cycle breakdown of the register-heap partial_sort select (kvc.hip
+// wave_heap_select) on one wave: the long-context h2o_attention case (k = 64 of 15 936, keys of
+// bf16 head sums, descending).  Tool, GPU box only:
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I include tools/heap_probe.hip \
+//       -o tools/heap_probe && tools/heap_probe
+// Prints per row: cycles of the whole select, and the number of elements that entered the heap
+// (pops) -- counted on the host by replaying the same scan against a host heap of keys.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "../cs3602-llm-inference-acceleration_amd/csrc/kvc.hip"
+
+constexpr int N = 15936, K = 64, ROWS = 32;
+
+__global__ void probe(const uint16_t* keys, uint16_t* out_idx, long long* cyc) {
+  __shared__ uint16_t key[N];
+  __shared__ uint16_t idx[N];
+  const uint16_t* kr = keys + (size_t)blockIdx.x * N;
+  for (int i = threadIdx.x; i < N; i += blockDim.x) {
+    key[i] = kr[i];
+    idx[i] = (uint16_t)i;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const long long t0 = __builtin_amdgcn_s_memtime();
+    kvc::wave_heap_select(key, idx, K, N);
+    const long long t1 = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+    out_idx[(size_t)blockIdx.x * K + threadIdx.x] = idx[threadIdx.x];
+  }
+}
+
+int main() {
+  std::mt19937 rng(7);
+  std::vector<uint16_t> keys((size_t)ROWS * N);
+  // keys of descending bf16 sums of 32 heads' softmax rows: emulate with bf16-rounded sums of
+  // 32 lognormal terms, complemented (desc) like the engine's key map
+  std::normal_distribution<float> nd(0.f, 1.f);
+  for (auto& k : keys) {
+    float s = 0.f;
+    for (int h = 0; h < 32; ++h) s += std::exp(nd(rng)) * 4e-5f;
+    uint32_t u;
+    memcpy(&u, &s, 4);
+    const uint16_t b = (uint16_t)((u + 0x7FFF + ((u >> 16) & 1)) >> 16);
+    k = (uint16_t)(0xFFFF - (0x8000 | b));  // desc key: larger sum -> smaller key
+  }
+  uint16_t *dk, *di;
+  long long* dc;
+  hipMalloc(&dk, keys.size() * 2);
+  hipMalloc(&di, ROWS * K * 2);
+  hipMalloc(&dc, ROWS * 8);
+  hipMemcpy(dk, keys.data(), keys.size() * 2, hipMemcpyHostToDevice);
+  for (int rep = 0; rep < 3; ++rep) hipLaunchKernelGGL(probe, dim3(ROWS), dim3(256), 0, 0, dk, di, dc);
+  hipDeviceSynchronize();
+  std::vector<long long> cyc(ROWS);
+  hipMemcpy(cyc.data(), dc, ROWS * 8, hipMemcpyDeviceToHost);
+  // pops per row: elements entering the heap (key < current max), host replay
+  long long pops_total = 0;
+  for (int r = 0; r < ROWS; ++r) {
+    std::vector<uint16_t> h(keys.begin() + (size_t)r * N, keys.begin() + (size_t)r * N + K);
+    std::make_heap(h.begin(), h.end());
+    for (int i = K; i < N; ++i) {
+      const uint16_t x = keys[(size_t)r * N + i];
+      if (x < h.front()) {
+        std::pop_heap(h.begin(), h.end());
+        h.back() = x;
+        std::push_heap(h.begin(), h.end());
+        ++pops_total;
+      }
+    }
+  }
+  // correctness: the kernel's slots = std::partial_sort's first k (key-only comparator: the same
+  // libstdc++ heap select), as sets
+  std::vector<uint16_t> got(ROWS * K);
+  hipMemcpy(got.data(), di, ROWS * K * 2, hipMemcpyDeviceToHost);
+  int bad = 0;
+  for (int r = 0; r < ROWS; ++r) {
+    std::vector<std::pair<uint16_t, uint16_t>> v(N);
+    for (int i = 0; i < N; ++i) v[i] = {keys[(size_t)r * N + i], (uint16_t)i};
+    std::partial_sort(v.begin(), v.begin() + K, v.end(),
+                      [](const auto& a, const auto& b) { return a.first < b.first; });
+    std::vector<uint16_t> want(K), have(got.begin() + r * K, got.begin() + (r + 1) * K);
+    for (int i = 0; i < K; ++i) want[i] = v[i].second;
+    std::sort(want.begin(), want.end());
+    std::sort(have.begin(), have.end());
+    bad += want != have;
+  }
+  printf("{\"rows_mismatching_partial_sort\": %d}\n", bad);
+  std::sort(cyc.begin(), cyc.end());
+  printf("{\"rows\": %d, \"n\": %d, \"k\": %d, \"cycles_median\": %lld, \"cycles_max\": %lld, "
+         "\"pops_per_row\": %.1f, \"cycles_per_pop\": %.1f}\n",
+         ROWS, N, K, cyc[ROWS / 2], cyc[ROWS - 1], pops_total / (double)ROWS,
+         cyc[ROWS / 2] / (pops_total / (double)ROWS));
+  return 0;
+}
