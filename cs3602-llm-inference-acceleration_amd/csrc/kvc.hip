@@ -182,6 +182,14 @@ __device__ __forceinline__ uint4 canon_nan_dt(uint4 a) {
   } while (0)
 #endif
 
+// Materialises x in a VGPR here: keeps the compiler from sinking the computation of a select
+// operand into an exec-mask branch (s_and_saveexec / s_or_b64 exec: scalar instructions on the
+// CU's one scalar unit, shared by all its waves) when only some lanes use it.
+__device__ __forceinline__ int vreg(int x) {
+  asm("" : "+v"(x));
+  return x;
+}
+
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -726,8 +734,10 @@ __device__ __forceinline__ void wave_stable_sort(KeyT* key, uint16_t* idx, int l
 // pop permutes one register instead of two (the children's keys and indices travel together).
 template <bool PACKED>
 struct RegHeap {
-  uint32_t hk;  // PACKED: key << 16 | index
-  uint32_t hi;  // !PACKED: index
+  uint32_t hk;   // PACKED: key << 16 | index
+  uint32_t hi;   // !PACKED: index
+  uint64_t anc;  // this slot and its ancestors below the root, as lane bits (fixed per lane)
+  int dep;       // this slot's depth
   __device__ __forceinline__ uint32_t key_of(uint32_t x) const { return PACKED ? x >> 16 : x; }
   __device__ __forceinline__ uint32_t k(int j) const {
     return key_of((uint32_t)__builtin_amdgcn_readlane((int)hk, j));
@@ -739,45 +749,65 @@ struct RegHeap {
   __device__ __forceinline__ void set(uint32_t key, uint32_t ix) {
     if constexpr (PACKED) hk = key << 16 | ix;
     else hk = key, hi = ix;
+    int a = (int)(threadIdx.x & 63), d = 0;
+    uint64_t m = 0;
+#pragma unroll
+    for (int st = 0; st < 6; ++st) {  // 64 slots: depth <= 6
+      m |= a > 0 ? 1ull << a : 0ull;
+      d += a > 0 ? 1 : 0;
+      a = a > 0 ? (a - 1) >> 1 : 0;
+    }
+    anc = m;
+    dep = d;
   }
-  // The path is found without a chase: every child lane learns from its sibling's key (a DPP
-  // wave shift, no LDS round trip) whether its parent chose it, one ballot collects those bits,
-  // and each lane walks its <= 6 ancestors in registers; each parent then pulls its chosen
-  // child's entry with one ds_bpermute issued as soon as the ballot is known.  (Round 3's
-  // readlane chase cost ~870 cycles per pop, tools/heap_probe.hip.)
+  // std::__adjust_heap + std::__push_heap from slot `top` with value (vk, vi), wave-parallel.
+  // The only serial chain is: sibling keys by DPP wave shifts -> "my parent chose me" bits ->
+  // one ballot B -> the path (each lane: are all links from top down to it in B, one mask test
+  // against its ancestor bits) -> m, one ballot.  Both children's entries are fetched with
+  // ds_bpermute at the start, off that chain.  (Round 3: a readlane chase of the path and
+  // bpermutes of the children's keys before it, ~630 cycles per pop in tools/heap_probe.hip.)
   __device__ __forceinline__ void adjust(int top, int len, uint32_t vk, uint32_t vi) {
     const int lane = (int)(threadIdx.x & 63);
+    const int c1 = min(2 * lane + 1, 63), c2 = min(2 * lane + 2, 63);
+    const uint32_t pl = (uint32_t)__builtin_amdgcn_ds_bpermute(c1 * 4, (int)hk);
+    const uint32_t pr = (uint32_t)__builtin_amdgcn_ds_bpermute(c2 * 4, (int)hk);
+    uint32_t il = 0, ir = 0;
+    if constexpr (!PACKED) {
+      il = (uint32_t)__builtin_amdgcn_ds_bpermute(c1 * 4, (int)hi);
+      ir = (uint32_t)__builtin_amdgcn_ds_bpermute(c2 * 4, (int)hi);
+    }
     const uint32_t key = key_of(hk);
     const uint32_t kn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key, 0x130, 0xF, 0xF, false);  // wave_shl:1: lane + 1
     const uint32_t kp = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)key, 0x138, 0xF, 0xF, false);  // wave_shr:1: lane - 1
     const int p = (lane - 1) >> 1;                              // parent of this lane
-    const bool two = p < (len - 1) / 2;                         // the parent has both children
-    const bool lone = (len & 1) == 0 && p == (len - 2) / 2;     // only the left one
-    // std::__adjust_heap: the right child unless it is strictly smaller than the left
-    const bool cb = lane >= 1 && lane < len &&
-                    ((lane & 1) ? (lone || (two && kn < key)) : (two && !(key < kp)));
-    const uint64_t B = __builtin_amdgcn_ballot_w64(cb);
-    const int c1 = min(2 * lane + 1, 63);
-    const int ch = ((B >> c1) & 1ull) ? c1 : min(2 * lane + 2, 63);  // chosen child (path nodes)
-    const uint32_t ck = (uint32_t)__builtin_amdgcn_ds_bpermute(ch * 4, (int)hk);
-    uint32_t ci = 0;
-    if constexpr (!PACKED) ci = (uint32_t)__builtin_amdgcn_ds_bpermute(ch * 4, (int)hi);
-    // on the path from `top` iff every link from top down to this lane is a chosen one
-    int a = lane, d = 0;
-    bool ok = lane >= top;
-#pragma unroll
-    for (int st = 0; st < 6; ++st) {  // heaps of <= 64 slots: depth <= 6
-      const bool step = a > top;
-      ok = ok && (!step || ((B >> a) & 1ull));
-      a = step ? (a - 1) >> 1 : a;
-      d += step ? 1 : 0;
+    // (bitwise, not short-circuit: && / || here compiled to exec-mask branches)
+    const unsigned two = p < (len - 1) / 2 ? 1u : 0u;           // the parent has both children
+    const unsigned lone = (len & 1) == 0 && p == (len - 2) / 2 ? 1u : 0u;  // only the left one
+    const unsigned in = lane >= 1 && lane < len ? 1u : 0u;
+    // the right child unless it is strictly smaller than the left (std::__adjust_heap)
+    const unsigned cl = lone | (two & (kn < key ? 1u : 0u));   // left child (odd lane) chosen
+    const unsigned cr = two & (key < kp ? 0u : 1u);             // right child (even lane) chosen
+    const uint64_t B = __builtin_amdgcn_ballot_w64((in & ((lane & 1) ? cl : cr)) != 0u);
+    // on the path from `top`: a descendant of top (or top) whose links below top are all in B
+    uint64_t links = anc;
+    int d = dep;
+    bool desc = true;
+    if (top != 0) {  // wave-uniform: make_heap's sift-downs
+      const uint64_t at = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)anc, top) |
+                          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(anc >> 32), top) << 32);
+      links = anc & ~at;
+      d = dep - __builtin_amdgcn_readlane(dep, top);
+      desc = (anc >> top) & 1ull;
     }
-    const bool onpath = ok && a == top;
-    const int m = __popcll(__builtin_amdgcn_ballot_w64(onpath && d >= 1 && !(key < vk)));
-    const bool up = onpath && d < m, here = onpath && d == m;
+    const unsigned onpath = desc && (B & links) == links ? 1u : 0u;
+    const int m = __popcll(__builtin_amdgcn_ballot_w64(
+        (onpath & (d >= 1 ? 1u : 0u) & (key < vk ? 0u : 1u)) != 0u));
+    const bool left = (B >> c1) & 1ull;  // this slot's chosen child (path slots above the leaf)
+    const uint32_t ck = (uint32_t)vreg((int)(left ? pl : pr));
+    const bool up = (onpath & (d < m ? 1u : 0u)) != 0u, here = (onpath & (d == m ? 1u : 0u)) != 0u;
     const uint32_t v = PACKED ? (vk << 16 | vi) : vk;
     hk = up ? ck : here ? v : hk;
-    if constexpr (!PACKED) hi = up ? ci : here ? vi : hi;
+    if constexpr (!PACKED) hi = up ? (uint32_t)vreg((int)(left ? il : ir)) : here ? vi : hi;
   }
 };
 
@@ -792,27 +822,36 @@ __device__ __forceinline__ void wave_heap_select(K* key, I* idx, int middle, int
       for (int parent = (middle - 2) / 2; parent >= 0; --parent)
         h.adjust(parent, middle, h.k(parent), h.i(parent));
     uint32_t top = h.k(0);
-    // the scan, four rows of 64 candidates per LDS round trip (the loads do not depend on the
-    // heap; only the ballots and pops do)
-    constexpr int R = 4;
+    // the scan, eight rows of 64 candidates per LDS round trip (the loads do not depend on the
+    // heap; only the ballots and pops do).  idx[i] == i on entry (both callers), so a candidate's
+    // index is its position.
+    constexpr int R = 8;
     for (int base = middle; base < len; base += 64 * R) {
-      uint32_t kq[R], iq[R];
+      uint32_t kq[R];
 #pragma unroll
       for (int q = 0; q < R; ++q) {
         const int i = base + q * 64 + lane;
         kq[q] = i < len ? (uint32_t)key[i] : 0xFFFFFFFFu;
-        iq[q] = i < len ? (uint32_t)idx[i] : 0u;
       }
+      // lanes past len hold ~0, never below top (16-bit keys are below 2^16); the rows' ballots
+      // against the current top first: most groups late in the row hold no candidate at all
+      uint64_t cm[R], any = 0;
 #pragma unroll
       for (int q = 0; q < R; ++q) {
-        // lanes past len hold ~0, never below top; 16-bit keys are below 2^16
-        uint64_t cand = __builtin_amdgcn_ballot_w64(kq[q] < top);
+        cm[q] = __builtin_amdgcn_ballot_w64(kq[q] < top);
+        any |= cm[q];
+      }
+      if (!any) continue;
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        // top only decreases: a row's candidates against the current top are a subset of cm[q]
+        uint64_t cand = cm[q] & __builtin_amdgcn_ballot_w64(kq[q] < top);
         while (cand) {
           const int l = (int)__builtin_ctzll(cand);
           // std::__pop_heap(first, middle, i): the old top goes to position i (never read again:
           // only the heap's slots are the result), element i sifts in from the root
           h.adjust(0, middle, (uint32_t)__builtin_amdgcn_readlane((int)kq[q], l),
-                   (uint32_t)__builtin_amdgcn_readlane((int)iq[q], l));
+                   (uint32_t)(base + q * 64 + l));
           top = h.k(0);
           cand &= ~((2ull << l) - 1ull) & __builtin_amdgcn_ballot_w64(kq[q] < top);
         }
@@ -888,14 +927,6 @@ __device__ __forceinline__ int vpopc(uint64_t m) {
 __device__ __forceinline__ int mbcnt(uint64_t mask, int base) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                         __builtin_amdgcn_mbcnt_lo((uint32_t)mask, (uint32_t)base));
-}
-
-// Materialises x in a VGPR here: keeps the compiler from sinking the computation of a select
-// operand into an exec-mask branch (s_and_saveexec / s_or_b64 exec: scalar instructions on the
-// CU's one scalar unit, shared by all its waves) when only some lanes use it.
-__device__ __forceinline__ int vreg(int x) {
-  asm("" : "+v"(x));
-  return x;
 }
 
 // f(integral_constant<int, I>) for I in [B, E): a loop the compiler cannot leave rolled.

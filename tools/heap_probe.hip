@@ -35,6 +35,24 @@ __global__ void probe(const uint16_t* keys, uint16_t* out_idx, long long* cyc) {
   }
 }
 
+// the adjust alone: NPOP pops of the root with values that always enter (decreasing keys)
+constexpr int NPOP = 1000;
+__global__ void pops_only(long long* cyc, uint32_t* sink) {
+  const int lane = threadIdx.x & 63;
+  kvc::RegHeap<true> h;
+  h.set(60000u - (uint32_t)lane, (uint32_t)lane);  // a valid max-heap? make it one below
+  for (int parent = (K - 2) / 2; parent >= 0; --parent) h.adjust(parent, K, h.k(parent), h.i(parent));
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  uint32_t v = 50000u;
+  for (int i = 0; i < NPOP; ++i) {
+    h.adjust(0, K, v, (uint32_t)i);
+    v -= 7u;
+  }
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) cyc[blockIdx.x] = t1 - t0;
+  sink[blockIdx.x * 64 + lane] = h.hk;
+}
+
 int main() {
   std::mt19937 rng(7);
   std::vector<uint16_t> keys((size_t)ROWS * N);
@@ -91,6 +109,28 @@ int main() {
     bad += want != have;
   }
   printf("{\"rows_mismatching_partial_sort\": %d}\n", bad);
+  {
+    uint32_t* ds;
+    hipMalloc(&ds, ROWS * 64 * 4);
+    hipLaunchKernelGGL(pops_only, dim3(ROWS), dim3(64), 0, 0, dc, ds);
+    hipLaunchKernelGGL(pops_only, dim3(ROWS), dim3(64), 0, 0, dc, ds);
+    hipDeviceSynchronize();
+    std::vector<long long> pc(ROWS);
+    hipMemcpy(pc.data(), dc, ROWS * 8, hipMemcpyDeviceToHost);
+    std::sort(pc.begin(), pc.end());
+    printf("{\"pops_only_cycles_per_pop\": %.1f}\n", pc[ROWS / 2] / (double)NPOP);
+  }
+  {  // the scan alone: nothing after the first k enters (larger keys), zero pops
+    std::vector<uint16_t> k2(keys.size());
+    for (size_t i = 0; i < k2.size(); ++i) k2[i] = (i % N) < K ? (uint16_t)(i % N) : (uint16_t)0xFFF0;
+    hipMemcpy(dk, k2.data(), k2.size() * 2, hipMemcpyHostToDevice);
+    for (int rep = 0; rep < 2; ++rep) hipLaunchKernelGGL(probe, dim3(ROWS), dim3(256), 0, 0, dk, di, dc);
+    hipDeviceSynchronize();
+    std::vector<long long> sc(ROWS);
+    hipMemcpy(sc.data(), dc, ROWS * 8, hipMemcpyDeviceToHost);
+    std::sort(sc.begin(), sc.end());
+    printf("{\"scan_only_cycles\": %lld}\n", sc[ROWS / 2]);
+  }
   std::sort(cyc.begin(), cyc.end());
   printf("{\"rows\": %d, \"n\": %d, \"k\": %d, \"cycles_median\": %lld, \"cycles_max\": %lld, "
          "\"pops_per_row\": %.1f, \"cycles_per_pop\": %.1f}\n",
