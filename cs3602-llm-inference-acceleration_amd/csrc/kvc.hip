@@ -1402,6 +1402,37 @@ __device__ __forceinline__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spo
   }
 }
 
+// Exclusive prefix sum of one int per thread over the NT threads of the block (wave scans as
+// four 16-lane DPP row scans, wave totals through `buf`); one barrier.
+template <int NT>
+__device__ __forceinline__ int block_exclusive_scan(int v, int* buf, int lane, int wid) {
+  static_assert(NT / 64 <= 16, "one 16-lane DPP row holds the wave totals");
+  const int rs = row_scan16(v);  // inclusive within each 16-lane row
+  const int r0 = __builtin_amdgcn_readlane(rs, 15), r1 = __builtin_amdgcn_readlane(rs, 31);
+  const int r2 = __builtin_amdgcn_readlane(rs, 47), r3 = __builtin_amdgcn_readlane(rs, 63);
+  const int row = lane >> 4;
+  const int excl = rs - v + (row > 0 ? r0 : 0) + (row > 1 ? r1 : 0) + (row > 2 ? r2 : 0);
+  if constexpr (NT == 64) {
+    return excl;
+  } else {
+    if (lane == 0) buf[wid] = r0 + r1 + r2 + r3;
+    __syncthreads();
+    const int ws = row_scan16(lane < NT / 64 ? buf[lane] : 0);
+    const int w = uni(wid);
+    return excl + (w ? __builtin_amdgcn_readlane(ws, w - 1) : 0);
+  }
+}
+
+
+// Atomic += 1 on an int in LDS (`p` a generic pointer into the workgroup's LDS: its low 32
+// bits are the LDS address).  A ds_add_u32 without return; callers wait (lgkmcnt) before the
+// barrier that publishes the sums.  (The compiler's own lowering of an atomic through such a
+// pointer emits an address-space test gfx950's VALU compare cannot encode.)
+__device__ __forceinline__ void lds_add1(int* p) {
+  const uint32_t a = (uint32_t)(uintptr_t)p;
+  asm volatile("ds_add_u32 %0, %1" ::"v"(a), "v"(1) : "memory");
+}
+
 // Block-wide sum of one int per wave (waves of NT threads).  Callers alternate two buffers, so
 // consecutive calls need one barrier each (a wave can only rewrite a buffer after every wave has
 // passed the barrier of the call in between, i.e. finished reading it).
@@ -1421,9 +1452,13 @@ __device__ __forceinline__ int block_sum_waves(int v, int* buf, int lane, int wi
 // the values alone.  fp32 norms essentially never tie at the boundary, so
 // this replaces the partition chain for them; bf16 / fp16 rows (tied in nearly every head) skip
 // it.  Returns true (and emits) when it applies.
+// With `radix`, `hist` (512 ints of LDS scratch: the rank tables, unused before the chain) T is found by
+// a radix select over the offsets key - min instead: 8-bit digits from the top, one 256-bin LDS
+// histogram of the keys still in the k-th key's bucket per digit (two buffers, each zeroed a pass
+// ahead), wave 0 locating the bucket -- two barriers per 8 bits instead of one per bit.
 template <int NT, int JM, typename KeyT, bool TO_LDS>
-__device__ bool select_fast_untied(const KeyT* key, int n, int k, SelScalars<KeyT>& sc,
-                                   int32_t* out, uint16_t* sel) {
+__device__ __forceinline__ bool select_fast_untied(const KeyT* key, int n, int k, SelScalars<KeyT>& sc,
+                                   int32_t* out, uint16_t* sel, int* hist, bool radix) {
   const int tid = threadIdx.x, lane = tid & 63, wid = (NT == 64) ? 0 : uni(tid >> 6);
   const int J = (n + NT - 1) / NT;
   if (J > JM) return false;
@@ -1460,9 +1495,60 @@ __device__ bool select_fast_untied(const KeyT* key, int n, int k, SelScalars<Key
   lo = (uint32_t)uni((int)lo);
   hi = (uint32_t)uni((int)hi);
   __syncthreads();  // sc.wa / sc.wb are the count buffers below
-  // smallest v with #(key <= v) >= k; invariant c_le = #(key <= hi) (= n at hi = max key)
   int c_le = n, parity = 0;
-  while (lo < hi) {
+  if (radix) {
+    const uint32_t span = hi - lo;
+    int rem = span ? 32 - __builtin_clz(span) : 0;  // offset bits still undecided
+    uint32_t prefix = 0;  // the decided high bits of the k-th key's offset
+    int below = 0;        // #keys whose offset lies below the bucket `prefix`
+    for (int i = tid; i < 512; i += NT) hist[i] = 0;
+    __syncthreads();
+    while (rem > 0) {
+      const int w = min(8, rem), sh = rem - w;
+      int* h = hist + 256 * parity;
+#pragma unroll
+      for (int j = 0; j < JM; ++j) {
+        const int pos = wbeg + j * 64 + lane;
+        const uint32_t d = kv[j] - lo;
+        if (j < J && pos < n && (uint32_t)((uint64_t)d >> rem) == prefix)
+          lds_add1(h + ((d >> sh) & ((1u << w) - 1u)));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // the other buffer's last reader (wave 0, previous pass) finished before the last barrier
+      for (int i = tid; i < 256; i += NT) hist[256 * (parity ^ 1) + i] = 0;
+      __syncthreads();
+      if (wid == 0) {
+        const int c0 = h[4 * lane], c1 = h[4 * lane + 1], c2 = h[4 * lane + 2],
+                  c3 = h[4 * lane + 3];
+        const int s4 = c0 + c1 + c2 + c3;
+        const int ex = block_exclusive_scan<64>(s4, nullptr, lane, 0);
+        const int need = k - below;  // >= 1: the k-th key lies in this bucket
+        const uint64_t b = __builtin_amdgcn_ballot_w64(ex + s4 >= need);
+        if (lane == (b ? __builtin_ctzll(b) : 63)) {
+          int c = ex, bin = 4 * lane, cnt = c0;
+          if (c + c0 < need) {
+            c += c0; ++bin; cnt = c1;
+            if (c + c1 < need) {
+              c += c1; ++bin; cnt = c2;
+              if (c + c2 < need) { c += c2; ++bin; cnt = c3; }
+            }
+          }
+          sc.wa[0] = bin;
+          sc.wb[0] = below + c;
+          sc.wm[0] = cnt;
+        }
+      }
+      __syncthreads();
+      prefix = (prefix << w) | (uint32_t)sc.wa[0];
+      below = sc.wb[0];
+      c_le = below + sc.wm[0];
+      rem = sh;
+      parity ^= 1;
+    }
+    lo = lo + prefix;
+  }
+  // smallest v with #(key <= v) >= k; invariant c_le = #(key <= hi) (= n at hi = max key)
+  while (!radix && lo < hi) {
     const uint32_t mid = lo + ((hi - lo) >> 1);
     int cl = 0;  // per-lane count (VALU), one wave reduction per step
 #pragma unroll
@@ -1518,27 +1604,6 @@ __device__ bool select_fast_untied(const KeyT* key, int n, int k, SelScalars<Key
 // global scratch row for zones longer than kZoneMax) and scalars in `sc`; NT threads (the
 // workgroup) cooperate.  Emits the kept zone-local indices in ascending order to `out` (global
 // int32) or, with TO_LDS, to `sel` (LDS u16, may alias the key region: keys are dead by then).
-// Exclusive prefix sum of one int per thread over the NT threads of the block (wave scans as
-// four 16-lane DPP row scans, wave totals through `buf`); one barrier.
-template <int NT>
-__device__ __forceinline__ int block_exclusive_scan(int v, int* buf, int lane, int wid) {
-  static_assert(NT / 64 <= 16, "one 16-lane DPP row holds the wave totals");
-  const int rs = row_scan16(v);  // inclusive within each 16-lane row
-  const int r0 = __builtin_amdgcn_readlane(rs, 15), r1 = __builtin_amdgcn_readlane(rs, 31);
-  const int r2 = __builtin_amdgcn_readlane(rs, 47), r3 = __builtin_amdgcn_readlane(rs, 63);
-  const int row = lane >> 4;
-  const int excl = rs - v + (row > 0 ? r0 : 0) + (row > 1 ? r1 : 0) + (row > 2 ? r2 : 0);
-  if constexpr (NT == 64) {
-    return excl;
-  } else {
-    if (lane == 0) buf[wid] = r0 + r1 + r2 + r3;
-    __syncthreads();
-    const int ws = row_scan16(lane < NT / 64 ? buf[lane] : 0);
-    const int w = uni(wid);
-    return excl + (w ? __builtin_amdgcn_readlane(ws, w - 1) : 0);
-  }
-}
-
 // Returns false (and ORs KVC_DEV_SELECT_BOUNDS into *status) when the row exceeds this kernel's
 // zone capacity -- nothing is selected then.
 template <int KC, bool TO_LDS, int MAXN, int NT>
@@ -1649,7 +1714,10 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
   // ---- reference-exact k-selection ----
   if constexpr (sizeof(KeyT) == 4 && MAXJ <= 16) {  // fp32 keys: untied boundary -> values only
     // (`sel` may alias the key region: the keys are read into registers before any store)
-    if (select_fast_untied<NT, MAXJ, KeyT, TO_LDS>(key, n, k, sc, out, sel)) {
+    // the rank tables (>= 2 KiB from n_cap = 1024 on) hold the radix histograms
+    const bool radix = (size_t)(cap + 72) * 4 >= 2048;
+    if (select_fast_untied<NT, MAXJ, KeyT, TO_LDS>(key, n, k, sc, out, sel,
+                                                   reinterpret_cast<int*>(idx + n_cap), radix)) {
       KVC_STAMP(31);  // diagnostic build: fast path taken
       return true;
     }
@@ -2617,11 +2685,14 @@ static int with_nc(int nc, F&& f) {
 
 // Keys are read once (non-temporal loads) and outputs written once (non-temporal stores): they
 // would otherwise evict useful lines from the Infinity Cache.
+#ifndef KVC_SCORE_TPW
+#define KVC_SCORE_TPW 1  // tiles per wave (A/B knob: a grid of 1/TPW the workgroups strides)
+#endif
 template <int DT, int NC>
 static int launch_score(const LayerChunk& T, int nl, int H, int64_t tile_base,
                         int64_t chunk_tiles, char* norms, int64_t nstride, hipStream_t s) {
-  constexpr int per_wg = score_waves(NC);  // one tile per wave
-  const unsigned grid = (unsigned)((chunk_tiles + per_wg - 1) / per_wg);
+  constexpr int per_wg = score_waves(NC);  // one tile per wave and grid stride
+  const unsigned grid = (unsigned)((chunk_tiles + per_wg * KVC_SCORE_TPW - 1) / (per_wg * KVC_SCORE_TPW));
   return launch_k(score_kernel<DT, NC, true>, dim3(grid), dim3(per_wg * 64), 0, s, T, nl, H,
                   tile_base, chunk_tiles, norms, nstride);
 }

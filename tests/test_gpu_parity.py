@@ -161,6 +161,24 @@ def test_abi_decode_tail_selections(dtype, variant):
             np.testing.assert_array_equal(idx, ref, err_msg=f"S={S} topk k={k}")
 
 
+@pytest.mark.parametrize("S", [900, 1024, 4097, 16384])
+@pytest.mark.parametrize("variant", ["normal", "few", "equal", "special", "tiny"])
+def test_abi_fp32_radix_fast_path(S, variant):
+    """fp32 keys: the untied fast path's radix select (from n_cap = 1024 on; rank tables hold its
+    histograms) -- untied rows ('normal', 'tiny': the set from the values alone) and rows whose
+    boundary ties ('few', 'equal') or whose key span covers all 32 bits ('special': NaN / inf
+    keys, four 8-bit digits) so the chain must run after the histograms used its tables."""
+    K = prng.gen_keys(6100 + S, (1, 2, S, 128), "fp32", variant)
+    for k in sorted({1, 2, S // 7, S // 2, S - 2, S - 1}):
+        for desc in (0, 1):
+            nrm, idx = _abi_select(K, k, desc, 0)
+            ref = np.sort(oracle.argsort_prefix(nrm, k, descending=bool(desc)), axis=-1)
+            np.testing.assert_array_equal(idx, ref, err_msg=f"S={S} sort k={k} desc={desc}")
+        nrm, idx = _abi_select(K, k, 1, 1)
+        ref = np.sort(oracle.topk_indices(nrm, k), axis=-1)
+        np.testing.assert_array_equal(idx, ref, err_msg=f"S={S} topk k={k}")
+
+
 def test_random_strategy_matches_torch_restatement():
     """strategy='random' consumes torch's device RNG exactly like the reference."""
     from kvcompress.methods import fix_size_l2_compress

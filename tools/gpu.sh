@@ -88,8 +88,8 @@ for step in "$@"; do
         for lib in ${AB_LIBS:?}; do
           for w in ${AB_WORKLOADS:-fix512-s16384}; do
             KVC_LIB="$LIBDIR/$lib" timeout -k 10 200 python bench.py --workload $w --steps 20 \
-                --warmup 5 --no-cpu-baseline > "$O/ab_one.json" 2> "$O/ab.err" || { tail "$O/ab.err"; exit 1; }
-            echo "{\"rep\": $rep, \"lib\": \"$lib\", \"workload\": \"$w\", \"r\": $(cat "$O/ab_one.json")}" >> "$O/ab.jsonl"
+                --warmup 5 --no-cpu-baseline $AB_ARGS > "$O/ab_one.json" 2> "$O/ab.err" || { tail "$O/ab.err"; exit 1; }
+            echo "{\"rep\": $rep, \"lib\": \"$lib\", \"workload\": \"$w\", \"args\": \"$AB_ARGS\", \"r\": $(cat "$O/ab_one.json")}" >> "$O/ab.jsonl"
           done
         done
       done

@@ -22,7 +22,8 @@ k = int(os.environ.get("SEL_K", "512"))
 ALGO = int(os.environ.get("SEL_ALGO", "0"))      # 1: topk (introselect)
 ORDER = int(os.environ.get("SEL_ORDER", "0"))    # 1: descending
 SCORE = int(os.environ.get("SEL_SCORE", "0"))    # 1: snapkv scoring (pool 5)
-DT = {"bf16": (torch.bfloat16, N.KVC_BF16), "fp16": (torch.float16, N.KVC_F16)}[os.environ.get("SEL_DTYPE", "bf16")]
+DT = {"bf16": (torch.bfloat16, N.KVC_BF16), "fp16": (torch.float16, N.KVC_F16),
+      "fp32": (torch.float32, N.KVC_F32)}[os.environ.get("SEL_DTYPE", "bf16")]
 Ks = [torch.randn(1, H, S, D, device=dev, generator=g).to(DT[0]) for _ in range(L)]
 table = np.zeros(L, dtype=N.LAYER_DTYPE)
 outs = []
@@ -71,6 +72,12 @@ for q, nm in enumerate(("P1", "P2", "P4")):
     res["block_level_" + nm + "_median"] = [float(np.median((sp[:, i] >> (20 * q)) & 0xFFFFF))
                                             for i in range(7)]
 print(json.dumps(res))
+if DT[1] == N.KVC_F32:  # untied fast path (slot 31 stamped when taken): key load, fast select
+    fast = allst[:, 31] > 0
+    print(json.dumps({"fp32_fast_path_rows": int(fast.sum()), "rows": rows,
+                      "key_load_median": float(np.median(allst[:, 1] - allst[:, 0])),
+                      "fast_select_median": float(np.median((allst[:, 31] - allst[:, 1])[fast]))
+                      if fast.any() else None}))
 if os.environ.get("SEL_P1_STAMPS"):  # diagnostic: level-0 P1 sub-phases (slots 26..29)
     ph = allst[:, 26:30].astype(np.float64)
     print(json.dumps({"level0_P1_phases_median": {
