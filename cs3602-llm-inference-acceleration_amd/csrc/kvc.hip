@@ -42,6 +42,8 @@ constexpr int kSelWaves = kSelThreads / 64;
 // with windows).  Longer zones keep 1 024 threads.
 constexpr int kSelThreadsSmall = 512;
 constexpr int kSmallZone = 8192;
+// occupancy the select kernels ask the compiler for (waves per SIMD)
+constexpr int sel_waves_per_eu(int kc, int nt) { return kc == KVC_F32 && nt == kSelThreads ? 4 : 8; }
 constexpr long kSmallBudget = 40448;  // 4 x (this + scalars) <= 160 KiB of LDS per CU
 constexpr long kBigBudget = 81408;    // 2 x (this + scalars) <= 160 KiB
 constexpr int kZoneMax = 16384;        // longest zone whose selection runs from LDS
@@ -1792,8 +1794,9 @@ constexpr int kSelCapBig = sel_cap(kZoneMax, (int)sizeof(KeyT), kBigBudget);
 template <typename KeyT>
 constexpr int kSelBytesBig = (int)sel_bytes(kZoneMax, (int)sizeof(KeyT), kSelCapBig<KeyT>);
 
+// 8 waves per SIMD: two 1024-thread rows per CU (fp32 rows of the big kernel: one per CU, LDS)
 template <int KC, int NT>
-__global__ void __launch_bounds__(NT, 8)  // 8 waves per SIMD: two 1024-thread rows per CU
+__global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT))
     select_kernel(const LayerChunk T, int BH, int dt, int order, int algo,
                   const char* __restrict__ norms, int64_t norm_stride,
                   int32_t* __restrict__ out_idx, int64_t idx_stride, int wave_seg, int n_cap,
@@ -2257,7 +2260,7 @@ __device__ __forceinline__ void gather_row(const kvc_layer_t* __restrict__ ly, i
 // counts as select_kernel; rows without a selection only copy.
 // ---------------------------------------------------------------------------------------------
 template <int KC, int NT, int NC>
-__global__ void __launch_bounds__(NT, 8)
+__global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT))
     select_gather_kernel(const LayerChunk T, int H, int BH, int dt, int order, int algo,
                          const char* __restrict__ norms, int64_t norm_stride, int wave_seg,
                          int n_cap, int cap, uint32_t* status) {
@@ -2685,14 +2688,11 @@ static int with_nc(int nc, F&& f) {
 
 // Keys are read once (non-temporal loads) and outputs written once (non-temporal stores): they
 // would otherwise evict useful lines from the Infinity Cache.
-#ifndef KVC_SCORE_TPW
-#define KVC_SCORE_TPW 1  // tiles per wave (A/B knob: a grid of 1/TPW the workgroups strides)
-#endif
 template <int DT, int NC>
 static int launch_score(const LayerChunk& T, int nl, int H, int64_t tile_base,
                         int64_t chunk_tiles, char* norms, int64_t nstride, hipStream_t s) {
-  constexpr int per_wg = score_waves(NC);  // one tile per wave and grid stride
-  const unsigned grid = (unsigned)((chunk_tiles + per_wg * KVC_SCORE_TPW - 1) / (per_wg * KVC_SCORE_TPW));
+  constexpr int per_wg = score_waves(NC);  // one tile per wave
+  const unsigned grid = (unsigned)((chunk_tiles + per_wg - 1) / per_wg);
   return launch_k(score_kernel<DT, NC, true>, dim3(grid), dim3(per_wg * 64), 0, s, T, nl, H,
                   tile_base, chunk_tiles, norms, nstride);
 }
