@@ -179,6 +179,26 @@ def test_abi_fp32_radix_fast_path(S, variant):
         np.testing.assert_array_equal(idx, ref, err_msg=f"S={S} topk k={k}")
 
 
+@pytest.mark.parametrize("S", [4096, 5000, 8192, 16384])
+@pytest.mark.parametrize("variant", ["normal", "few", "equal", "special", "ramp"])
+def test_abi_heap_select_candidate_prefilter(S, variant):
+    """std::partial_sort's heap select (topk with k * 64 <= n) on rows of >= 4 096 positions:
+    waves 1.. prefilter the positions that can enter the heap while wave 0 builds it (512-thread
+    rows up to 8 192 positions, 1 024-thread rows beyond).  'ramp': norms rising along the row,
+    so every position enters the heap -- more candidates than the rank tables hold, the full
+    scan runs instead."""
+    if variant == "ramp":
+        K = np.zeros((1, 2, S, 128), dtype=np.float32)
+        K[0, :, :, 0] = (np.arange(S, dtype=np.float32) + 1.0)[None, :]
+        K = prng.to_dtype(K, "bf16")
+    else:
+        K = prng.gen_keys(7300 + S, (1, 2, S, 128), "bf16", variant)
+    for k in (1, 2, 17, 63, 64):
+        nrm, idx = _abi_select(K, k, 1, 1)
+        ref = np.sort(oracle.topk_indices(nrm, k), axis=-1)
+        np.testing.assert_array_equal(idx, ref, err_msg=f"S={S} topk k={k}")
+
+
 def test_random_strategy_matches_torch_restatement():
     """strategy='random' consumes torch's device RNG exactly like the reference."""
     from kvcompress.methods import fix_size_l2_compress

@@ -3,7 +3,8 @@ passes (tools/gpu.sh pmc) -> profiles/<name>_pmc_traffic.json.
 
 FETCH_SIZE / WRITE_SIZE are KiB.  On gfx950 FETCH_SIZE sees only half of wide coalesced read
 streams (MI355X_MICROARCH.md, HBM / rocprofv3 section), so FETCH x2 is the HBM read estimate.
-Usage: python tools/pmc_traffic.py gpurun_out profiles/r01_v6_pmc_traffic.json"""
+Usage: python tools/pmc_traffic.py gpurun_out profiles/r01_v6_pmc_traffic.json
+(PMC_S / PMC_D: another fix_size_l2 workload's sequence length / head dim)"""
 import csv
 import json
 import os
@@ -12,7 +13,9 @@ import sys
 from collections import defaultdict
 
 src, dst = sys.argv[1], sys.argv[2]
-L, H, S, D, K = 32, 32, 16384, 128, 512
+L, H, K = 32, 32, 512
+S = int(os.environ.get("PMC_S", "16384"))  # the workload's geometry (default: the headline)
+D = int(os.environ.get("PMC_D", "128"))
 ALGO = {  # bytes per 32-layer launch of the headline workload
     "score_kernel": {"algorithmic_read": L * H * S * D * 2, "algorithmic_write": L * H * S * 2},
     "gather_kernel": {"algorithmic_read": 2 * L * H * K * D * 2,
