@@ -181,12 +181,10 @@ def test_abi_fp32_radix_fast_path(S, variant):
 
 @pytest.mark.parametrize("S", [4096, 5000, 8192, 16384])
 @pytest.mark.parametrize("variant", ["normal", "few", "equal", "special", "ramp"])
-def test_abi_heap_select_candidate_prefilter(S, variant):
-    """std::partial_sort's heap select (topk with k * 64 <= n) on rows of >= 4 096 positions:
-    waves 1.. prefilter the positions that can enter the heap while wave 0 builds it (512-thread
-    rows up to 8 192 positions, 1 024-thread rows beyond).  'ramp': norms rising along the row,
-    so every position enters the heap -- more candidates than the rank tables hold, the full
-    scan runs instead."""
+def test_abi_heap_select_long_rows(S, variant):
+    """std::partial_sort's heap select (topk with k * 64 <= n) on rows of >= 4 096 positions
+    (512-thread rows up to 8 192 positions, 1 024-thread rows beyond).  'ramp': norms rising
+    along the row, so every position enters the heap (a pop per position)."""
     if variant == "ramp":
         K = np.zeros((1, 2, S, 128), dtype=np.float32)
         K[0, :, :, 0] = (np.arange(S, dtype=np.float32) + 1.0)[None, :]
