@@ -43,7 +43,10 @@ constexpr int kSelWaves = kSelThreads / 64;
 constexpr int kSelThreadsSmall = 512;
 constexpr int kSmallZone = 8192;
 // occupancy the select kernels ask the compiler for (waves per SIMD)
-constexpr int sel_waves_per_eu(int kc, int nt) { return kc == KVC_F32 && nt == kSelThreads ? 4 : 8; }
+// (the heavy-hitter select kernels run one row per CU: no occupancy target to spill for)
+constexpr int sel_waves_per_eu(int kc, int nt, bool hh = false) {
+  return hh || (kc == KVC_F32 && nt == kSelThreads) ? 4 : 8;
+}
 constexpr long kSmallBudget = 40448;  // 4 x (this + scalars) <= 160 KiB of LDS per CU
 constexpr long kBigBudget = 81408;    // 2 x (this + scalars) <= 160 KiB
 constexpr int kZoneMax = 16384;        // longest zone whose selection runs from LDS
@@ -813,56 +816,80 @@ struct RegHeap {
   }
 };
 
+// The register heap of wave_heap_select (middle <= 64), in two steps so that a block can build
+// it in one wave while its other waves prefilter the candidates (heap_candidates):
+// std::make_heap over the first `middle` slots ...
+template <bool PK, typename K, typename I>
+__device__ __forceinline__ void reg_heap_make(RegHeap<PK>& h, const K* key, const I* idx,
+                                              int middle) {
+  const int lane = threadIdx.x & 63;
+  h.set(lane < middle ? (uint32_t)key[lane] : 0u, lane < middle ? (uint32_t)idx[lane] : 0u);
+  if (middle >= 2)
+    for (int parent = (middle - 2) / 2; parent >= 0; --parent)
+      h.adjust(parent, middle, h.k(parent), h.i(parent));
+}
+// ... then the scan of positions [middle, len) -- or only the ascending candidate positions
+// `cand[0..ncand)` -- with its pops, and the heap's slots stored to key / idx[0..middle).
+template <bool PK, typename K, typename I>
+__device__ __forceinline__ void reg_heap_scan(RegHeap<PK>& h, K* key, I* idx, int middle, int len,
+                                              const uint16_t* cand, int ncand) {
+  const int lane = threadIdx.x & 63;
+  uint32_t top = h.k(0);
+  // the scan, eight rows of 64 candidates per LDS round trip (the loads do not depend on the
+  // heap; only the ballots and pops do).  idx[i] == i on entry (every caller), so a candidate's
+  // index is its position.
+  constexpr int R = 8;
+  const int end = cand ? ncand : len, first = cand ? 0 : middle;
+  for (int base = first; base < end; base += 64 * R) {
+    uint32_t kq[R], pq[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int i = base + q * 64 + lane;
+      pq[q] = cand ? (uint32_t)cand[min(i, end - 1)] : (uint32_t)i;
+    }
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int i = base + q * 64 + lane;
+      kq[q] = i < end ? (uint32_t)key[pq[q]] : 0xFFFFFFFFu;
+    }
+    // lanes past the end hold ~0, never below top (16-bit keys are below 2^16); the rows'
+    // ballots against the current top first: most groups late in the row hold no candidate
+    uint64_t cm[R], any = 0;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      cm[q] = __builtin_amdgcn_ballot_w64(kq[q] < top);
+      any |= cm[q];
+    }
+    if (!any) continue;
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      // top only decreases: a row's candidates against the current top are a subset of cm[q]
+      uint64_t c = cm[q] & __builtin_amdgcn_ballot_w64(kq[q] < top);
+      while (c) {
+        const int l = (int)__builtin_ctzll(c);
+        // std::__pop_heap(first, middle, i): the old top goes to position i (never read again:
+        // only the heap's slots are the result), element i sifts in from the root
+        h.adjust(0, middle, (uint32_t)__builtin_amdgcn_readlane((int)kq[q], l),
+                 (uint32_t)__builtin_amdgcn_readlane((int)pq[q], l));
+        top = h.k(0);
+        c &= ~((2ull << l) - 1ull) & __builtin_amdgcn_ballot_w64(kq[q] < top);
+      }
+    }
+  }
+  if (lane < middle) {
+    key[lane] = (K)h.key_of(h.hk);
+    idx[lane] = (I)(PK ? (h.hk & 0xFFFFu) : h.hi);
+  }
+}
+
 template <typename K, typename I>
 __device__ __forceinline__ void wave_heap_select(K* key, I* idx, int middle, int len) {
   const int lane = threadIdx.x & 63;
   if (middle <= 64) {  // the heap in registers (RegHeap): make_heap, then the scan with its pops
     constexpr bool PK = sizeof(K) == 2 && sizeof(I) == 2;
     RegHeap<PK> h;
-    h.set(lane < middle ? (uint32_t)key[lane] : 0u, lane < middle ? (uint32_t)idx[lane] : 0u);
-    if (middle >= 2)
-      for (int parent = (middle - 2) / 2; parent >= 0; --parent)
-        h.adjust(parent, middle, h.k(parent), h.i(parent));
-    uint32_t top = h.k(0);
-    // the scan, eight rows of 64 candidates per LDS round trip (the loads do not depend on the
-    // heap; only the ballots and pops do).  idx[i] == i on entry (both callers), so a candidate's
-    // index is its position.
-    constexpr int R = 8;
-    for (int base = middle; base < len; base += 64 * R) {
-      uint32_t kq[R];
-#pragma unroll
-      for (int q = 0; q < R; ++q) {
-        const int i = base + q * 64 + lane;
-        kq[q] = i < len ? (uint32_t)key[i] : 0xFFFFFFFFu;
-      }
-      // lanes past len hold ~0, never below top (16-bit keys are below 2^16); the rows' ballots
-      // against the current top first: most groups late in the row hold no candidate at all
-      uint64_t cm[R], any = 0;
-#pragma unroll
-      for (int q = 0; q < R; ++q) {
-        cm[q] = __builtin_amdgcn_ballot_w64(kq[q] < top);
-        any |= cm[q];
-      }
-      if (!any) continue;
-#pragma unroll
-      for (int q = 0; q < R; ++q) {
-        // top only decreases: a row's candidates against the current top are a subset of cm[q]
-        uint64_t cand = cm[q] & __builtin_amdgcn_ballot_w64(kq[q] < top);
-        while (cand) {
-          const int l = (int)__builtin_ctzll(cand);
-          // std::__pop_heap(first, middle, i): the old top goes to position i (never read again:
-          // only the heap's slots are the result), element i sifts in from the root
-          h.adjust(0, middle, (uint32_t)__builtin_amdgcn_readlane((int)kq[q], l),
-                   (uint32_t)(base + q * 64 + l));
-          top = h.k(0);
-          cand &= ~((2ull << l) - 1ull) & __builtin_amdgcn_ballot_w64(kq[q] < top);
-        }
-      }
-    }
-    if (lane < middle) {
-      key[lane] = (K)h.key_of(h.hk);
-      idx[lane] = (I)(PK ? (h.hk & 0xFFFFu) : h.hi);
-    }
+    reg_heap_make(h, key, idx, middle);
+    reg_heap_scan(h, key, idx, middle, len, nullptr, 0);
     wave_sync();
     return;
   }
@@ -984,6 +1011,89 @@ __device__ __forceinline__ void p1_counts(const KeyT* key, int pos0, int J, int 
                        (uint32_t)__builtin_amdgcn_readlane(rs, 63);
   cge += (int)(tot & 0xFFFFu);
   cle += (int)(tot >> 16);
+}
+
+// Candidate prefilter of std::__heap_select(first, middle, last) for middle <= 64, by NT
+// threads: position i >= middle enters the heap iff key[i] < top_i, and top_i -- the heap's max
+// -- is the middle-th smallest key of [0, i) (the heap always holds the `middle` smallest keys
+// seen, as a multiset).  Any `middle`-element subset of [0, i) bounds it from above, so with the
+// scan range cut into one chunk per wave, U_w = min(max of the first `middle` keys, the
+// middle-th smallest key of each earlier chunk) >= top_i for every i of chunk w, and {i in chunk
+// w : key[i] < U_w} holds every entering position.  Writes those positions, ascending, to `cand`
+// (capacity ccap) and returns their count, or -1 (nothing written) when they do not fit or a
+// chunk exceeds 20 rows of 64; ends with a barrier.  The heap scan then visits only them:
+// ~1 800 of 15 936 positions for the h2o heavy hitters (k = 64).
+template <int NT, bool EXACT = true, typename K>
+__device__ int heap_candidates(const K* key, int middle, int len, uint16_t* cand, int ccap,
+                               int* wbuf, int* cbuf, int w0 = 0) {
+  constexpr int NW = NT / 64, JM = 20;  // 16 384 positions over 15 chunk waves: 17 rows
+  static_assert(NW <= 16, "one 16-lane DPP row holds the wave values");
+  const int lane = threadIdx.x & 63, wid = uni((int)(threadIdx.x >> 6));
+  const int span = len - middle;
+  const int rows = (span + 64 * (NW - w0) - 1) / (64 * (NW - w0));  // rows per chunk (uniform)
+  if (rows > JM) return -1;
+  // waves below w0 (busy elsewhere until the first barrier) hold no chunk
+  const int c0 = wid < w0 ? len : middle + (wid - w0) * rows * 64, c1 = min(c0 + rows * 64, len);
+  uint32_t kv[JM];
+  uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+    const int pos = c0 + j * 64 + lane;
+    const bool v = j < rows && pos < c1;
+    kv[j] = v ? (uint32_t)key[pos] : 0xFFFFFFFFu;
+    mn = v ? min(mn, kv[j]) : mn;
+    mx = v ? max(mx, kv[j]) : mx;
+  }
+  uint32_t q0 = lane < middle ? (uint32_t)key[lane] : 0u;  // max of the first `middle` keys
+  if (!EXACT) mx = mn;  // loose bound: the largest lane minimum (>= 64 keys lie at or below it)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    if (EXACT) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+    q0 = max(q0, (uint32_t)__shfl_xor((int)q0, o, 64));
+  }
+  // this chunk's middle-th smallest key: the smallest v with #(key <= v) >= middle (bisection on
+  // the VALU, one wave reduction per step); loose: every lane holds a key (a full first row)
+  uint32_t lo = EXACT ? (uint32_t)uni((int)mn) : (uint32_t)uni((int)mx), hi = (uint32_t)uni((int)mx);
+  const bool has = EXACT ? c1 - c0 >= middle : c1 - c0 >= 64;
+  while (EXACT && has && lo < hi) {
+    const uint32_t mid = lo + ((hi - lo) >> 1);
+    int cl = 0;
+#pragma unroll
+    for (int j = 0; j < JM; ++j) cl += kv[j] <= mid ? 1 : 0;  // invalid slots hold ~0u
+    const int rs = row_scan16(cl);
+    const int c = __builtin_amdgcn_readlane(rs, 15) + __builtin_amdgcn_readlane(rs, 31) +
+                  __builtin_amdgcn_readlane(rs, 47) + __builtin_amdgcn_readlane(rs, 63);
+    if (c >= middle) hi = mid;
+    else lo = mid + 1;
+  }
+  if (lane == 0) wbuf[wid] = has ? (int)lo : -1;  // -1: no bound (0xFFFFFFFF)
+  __syncthreads();
+  uint32_t U = (uint32_t)uni((int)q0);
+  for (int w = 0; w < wid; ++w) U = min(U, (uint32_t)wbuf[w]);
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < JM; ++j) c += __popcll(__builtin_amdgcn_ballot_w64(kv[j] < U));
+  if (lane == 0) cbuf[wid] = c;
+  __syncthreads();
+  int before = 0, total = 0;
+  for (int w = 0; w < NW; ++w) {
+    const int cw = cbuf[w];
+    before += w < wid ? cw : 0;
+    total += cw;
+  }
+  if (total > ccap) {
+    __syncthreads();  // wbuf / cbuf are free again
+    return -1;
+  }
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+    const uint64_t b = __builtin_amdgcn_ballot_w64(kv[j] < U);
+    if (kv[j] < U) cand[before + mbcnt(b, 0)] = (uint16_t)(c0 + j * 64 + lane);
+    before += __popcll(b);
+  }
+  __syncthreads();
+  return total;
 }
 
 // P2 of a level, rank window 0: scatter the s and g rank -> position tables for ranks <= cap
@@ -1608,7 +1718,7 @@ __device__ __forceinline__ bool select_fast_untied(const KeyT* key, int n, int k
 // int32) or, with TO_LDS, to `sel` (LDS u16, may alias the key region: keys are dead by then).
 // Returns false (and ORs KVC_DEV_SELECT_BOUNDS into *status) when the row exceeds this kernel's
 // zone capacity -- nothing is selected then.
-template <int KC, bool TO_LDS, int MAXN, int NT>
+template <int KC, bool TO_LDS, int MAXN, int NT, bool HH = false>
 __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, int dt, int order,
                             int algo, const char* __restrict__ nrow, int32_t* out, uint16_t* sel,
                             char* arrays, int n_cap, int cap,
@@ -1724,8 +1834,22 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
       return true;
     }
   }
-  if (partial) {
-    if (wid == 0) wave_heap_select(key, idx, k, n);  // std::partial_sort's heap select
+  if (partial) {  // std::partial_sort's heap select
+    bool done = false;
+    if constexpr (HH && NT > 64) {  // heavy-hitter kernels only: see heap_candidates
+      if (k <= 64 && n >= 4096) {
+        // wave 0 builds the register heap while the other waves prefilter the scan's candidates
+        // into the rank tables (unused by the heap select); then wave 0 scans only those
+        constexpr bool PK = sizeof(KeyT) == 2;
+        RegHeap<PK> h;
+        if (wid == 0) reg_heap_make(h, key, idx, k);
+        uint16_t* cand = idx + n_cap;
+        const int nc = heap_candidates<NT>(key, k, n, cand, (cap + 72) * 2, sc.wa, sc.wb, 1);
+        if (wid == 0) reg_heap_scan(h, key, idx, k, n, nc >= 0 ? cand : nullptr, nc);
+        done = true;
+      }
+    }
+    if (!done && wid == 0) wave_heap_select(key, idx, k, n);
   } else {
     int lo = 0, hi = n, depth = 2 * floor_log2(n), level = 0;
     uint64_t* accb = nullptr;
@@ -1794,9 +1918,10 @@ constexpr int kSelCapBig = sel_cap(kZoneMax, (int)sizeof(KeyT), kBigBudget);
 template <typename KeyT>
 constexpr int kSelBytesBig = (int)sel_bytes(kZoneMax, (int)sizeof(KeyT), kSelCapBig<KeyT>);
 
-// 8 waves per SIMD: two 1024-thread rows per CU (fp32 rows of the big kernel: one per CU, LDS)
-template <int KC, int NT>
-__global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT))
+// 8 waves per SIMD: two 1024-thread rows per CU (fp32 rows of the big kernel: one per CU, LDS).
+// HH: the heavy-hitter instance (kvc_heavy_hitters), whose heap selects prefilter their scan.
+template <int KC, int NT, bool HH = false>
+__global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT, HH))
     select_kernel(const LayerChunk T, int BH, int dt, int order, int algo,
                   const char* __restrict__ norms, int64_t norm_stride,
                   int32_t* __restrict__ out_idx, int64_t idx_stride, int wave_seg, int n_cap,
@@ -1810,13 +1935,13 @@ __global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT))
   if constexpr (NT == kSelThreads) {
     // LDS: key[kZoneMax] | idx[kZoneMax] (u16) | spos | gpos (u16 rank windows) -- SelArrays
     __shared__ __attribute__((aligned(16))) char smem[kSelBytesBig<KeyT>];
-    select_body<KC, false, MAXN, NT>(ly, dt, order, algo,
+    select_body<KC, false, MAXN, NT, HH>(ly, dt, order, algo,
                                      norms + (int64_t)row * norm_stride * ESZ,
                                      out_idx + (int64_t)row * idx_stride, nullptr, smem, kZoneMax,
                                      kSelCapBig<KeyT>, sc, wave_seg, stamps, status);
   } else {
     extern __shared__ __attribute__((aligned(16))) char dsmem[];
-    select_body<KC, false, MAXN, NT>(ly, dt, order, algo,
+    select_body<KC, false, MAXN, NT, HH>(ly, dt, order, algo,
                                      norms + (int64_t)row * norm_stride * ESZ,
                                      out_idx + (int64_t)row * idx_stride, nullptr, dsmem, n_cap,
                                      cap, sc, wave_seg, stamps, status);
@@ -2716,7 +2841,7 @@ static int launch_gather(const LayerChunk& T, int nl, int H, int BH, const int32
 // SELECT over the rows of a chunk (BH rows per layer, workspace row ly->row0 + blockIdx % BH):
 // the LDS kernels (512-thread rows for zones up to kSmallZone, else 1 024-thread rows) or, for
 // zones longer than kZoneMax, the global-scratch kernels (u32 positions beyond kZoneMaxGlobal).
-template <int KC>
+template <int KC, bool HH = false>
 static int launch_select(const LayerChunk& T, int cn, int BH, int dt, int order, int algo,
                          const char* norms, int64_t nstride, int32_t* idx, int64_t istride,
                          bool long_zone, char* scratch, uint64_t* stamps, uint32_t* status,
@@ -2736,11 +2861,11 @@ static int launch_select(const LayerChunk& T, int cn, int BH, int dt, int order,
   const int ks = (int)sizeof(KeyT);
   if (n_cap <= kSmallZone) {
     const int cap = sel_cap(n_cap, ks, kSmallBudget);
-    return launch_k(select_kernel<KC, kSelThreadsSmall>, rows_grid, dim3(kSelThreadsSmall),
+    return launch_k(select_kernel<KC, kSelThreadsSmall, HH>, rows_grid, dim3(kSelThreadsSmall),
                     sel_bytes(n_cap, ks, cap), s, T, BH, dt, order, algo, norms, nstride, idx,
                     istride, kWaveSegSmall, n_cap, cap, stamps, status);
   }
-  return launch_k(select_kernel<KC, kSelThreads>, rows_grid, dim3(kSelThreads), 0, s, T, BH, dt,
+  return launch_k(select_kernel<KC, kSelThreads, HH>, rows_grid, dim3(kSelThreads), 0, s, T, BH, dt,
                   order, algo, norms, nstride, idx, istride, kWaveSeg, n_cap, 0, stamps, status);
 }
 
@@ -2971,7 +3096,7 @@ static int heavy_hitters_impl(const kvc_attn_params_t* p, const kvc_hh_layer_t* 
                        vec_min, sums, nstride);
       if (r != KVC_OK) return r;
       // torch.topk(largest=True) + torch.sort: the descending TOPK selection, ascending indices
-      return launch_select<KC>(S, cn, B, DT, KVC_DESC, KVC_ALGO_TOPK, sums, nstride, o, ostride,
+      return launch_select<KC, true>(S, cn, B, DT, KVC_DESC, KVC_ALGO_TOPK, sums, nstride, o, ostride,
                                long_zone, scratch, nullptr, p->device_status, s);
     });
   }
