@@ -97,6 +97,7 @@ def test_engine_matches_torch_cpu_ops(threads, dt):
                                 (1, 4, [(5, 100), (17, 120)], 8),
                                 (1, 1, [(2, 3000), (1, 3001)], 32),
                                 (2, 16, [(9, 1100), (1, 1101)], 40),
+                                (1, 8, [(1, 6000)], 64),  # heap select, 512-thread rows
                                 (1, 32, [(1, 16384)], 64)]:  # heap select over 16 330
             mgr = H2OAttentionManager(start_size=4, heavy_hitter_size=hh, recent_size=50,
                                       decay_factor=0.9)
