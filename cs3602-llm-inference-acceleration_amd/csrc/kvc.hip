@@ -1645,15 +1645,17 @@ __device__ __forceinline__ bool select_fast_untied(const KeyT* key, int n, int k
               if (c + c2 < need) { c += c2; ++bin; cnt = c3; }
             }
           }
+          // published in slots the emission below never writes (it writes sc.wm[wid] while a
+          // lagging wave may still read this pass's values)
           sc.wa[0] = bin;
           sc.wb[0] = below + c;
-          sc.wm[0] = cnt;
+          sc.fnan[0] = cnt;
         }
       }
       __syncthreads();
       prefix = (prefix << w) | (uint32_t)sc.wa[0];
       below = sc.wb[0];
-      c_le = below + sc.wm[0];
+      c_le = below + sc.fnan[0];
       rem = sh;
       parity ^= 1;
     }
@@ -2703,6 +2705,11 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
   if ((p->flags & KVC_FLAG_GATHER_FIXED) && (p->flags & KVC_FLAG_GATHER_SELECTED))
     return KVC_E_ARG;
   if ((p->flags & KVC_FLAG_SHARED_INDEX) && !p->external_index) return KVC_E_ARG;
+  // the two gather parts of one call share its index region: with the engine's own selection
+  // each launch would also SCORE and SELECT into the same workspace (a race when the two run
+  // concurrently, as the flags intend) -- so only external indices may be split
+  if ((p->flags & (KVC_FLAG_GATHER_FIXED | KVC_FLAG_GATHER_SELECTED)) && !p->external_index)
+    return KVC_E_ARG;
   const int es = esize(p->dtype);
   const int rowb = p->head_dim * es;
   if (rowb % 16) return KVC_E_HEADDIM;

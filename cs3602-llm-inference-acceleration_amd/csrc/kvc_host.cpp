@@ -352,10 +352,33 @@ py::tuple run_h2o(py::list kv, py::object attns, py::list accs, std::vector<int6
                                (int)na, reinterpret_cast<kvc_stream_t>(stream));
   if (rc != KVC_OK)
     throw std::runtime_error(std::string("kvc_attn_accumulate failed: ") + kvc_status_string(rc));
+  // Joins the side stream back into `main` on every exit path once the side copy is enqueued:
+  // if a later launch throws, the outputs it writes are freed to the caching allocator (on
+  // `main`) only after the copy has finished.
+  struct Join {
+    const SideStream* s = nullptr;
+    hipStream_t main;
+    bool armed = false;
+    void operator()() {
+      if (!armed) return;
+      armed = false;
+      check_hip(hipEventRecord(s->join, s->side), "hipEventRecord");
+      check_hip(hipStreamWaitEvent(main, s->join, 0), "hipStreamWaitEvent");
+    }
+    ~Join() {
+      if (armed) {  // unwinding: best effort, never throw from a destructor
+        (void)hipEventRecord(s->join, s->side);
+        (void)hipStreamWaitEvent(main, s->join, 0);
+      }
+    }
+  } join;
+  join.main = main;
   if (fixed_params && !o.table.empty()) {  // the sink / recent rows, beside the heavy hitters
     side = &side_stream();
+    join.s = side;
     check_hip(hipEventRecord(side->fork, main), "hipEventRecord");
     check_hip(hipStreamWaitEvent(side->side, side->fork, 0), "hipStreamWaitEvent");
+    join.armed = true;
     launch(o, fixed_params, ws, ws_bytes, reinterpret_cast<int64_t>(side->side));
   }
   const size_t nh = hh_rows.size();
@@ -373,10 +396,7 @@ py::tuple run_h2o(py::list kv, py::object attns, py::list accs, std::vector<int6
   if (rc != KVC_OK)
     throw std::runtime_error(std::string("kvc_heavy_hitters failed: ") + kvc_status_string(rc));
   launch(o, side ? sel_params : params_addr, ws, ws_bytes, stream);
-  if (side) {
-    check_hip(hipEventRecord(side->join, side->side), "hipEventRecord");
-    check_hip(hipStreamWaitEvent(main, side->join, 0), "hipStreamWaitEvent");
-  }
+  join();
   return py::make_tuple(result_list(kv.ptr(), ks, vs, act, o), acc_out);
 }
 

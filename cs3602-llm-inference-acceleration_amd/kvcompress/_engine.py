@@ -366,6 +366,51 @@ def device_status(device=None, clear=False):
     return v
 
 
+# Opt-in production check of the device status word: after every compress call (and every
+# h2o_attention manager call) the words of the devices the engine has used are read -- one
+# synchronisation per call -- and a non-zero word is cleared and raised as RuntimeError naming its
+# bits.  Off by default (the read synchronises the device); KVC_CHECK_STATUS=1 in the environment
+# turns it on at import, set_status_check() at run time.
+import os as _os
+
+check_status = _os.environ.get("KVC_CHECK_STATUS", "") not in ("", "0")
+
+_STATUS_BITS = ((N.DEV_SELECT_BOUNDS, "KVC_DEV_SELECT_BOUNDS (a selection row exceeded its "
+                 "kernel's zone capacity: that row's output was left unwritten)"),
+                (N.DEV_INDEX_RANGE, "KVC_DEV_INDEX_RANGE (a caller-provided index lay outside its "
+                 "zone and was clamped)"))
+
+
+def set_status_check(on: bool = True):
+    """Turn the per-call device status check on or off; returns the previous setting."""
+    global check_status
+    prev, check_status = check_status, bool(on)
+    return prev
+
+
+def raise_on_status():
+    """Read (and clear) every used device's status word; RuntimeError if any bit is set."""
+    for device in list(_status_words):
+        v = device_status(device, clear=True)
+        if v:
+            names = [txt for bit, txt in _STATUS_BITS if v & bit] or [f"unknown bits {v:#x}"]
+            raise RuntimeError(f"kvcompress (MI355X HIP engine): cuda:{device} reported "
+                               f"device status {v:#x}: " + "; ".join(names))
+
+
+def status_checked(fn):
+    """Wrap an entry point so that, with check_status on, its calls end with raise_on_status()."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrapper(*args, **kwargs):
+        out = fn(*args, **kwargs)
+        if check_status:
+            raise_on_status()
+        return out
+    return wrapper
+
+
 def _params(dtype, B, H, D, order, algo, external, shared=False):
     flags = (N.FLAG_SPLIT_SELECT_GATHER if split_select_gather else 0) | \
         (N.FLAG_SHARED_INDEX if shared else 0)
@@ -537,12 +582,16 @@ def execute_shared(jobs: List[Segments], out_list: list, fill, overlap=False):
                 p.flags |= N.FLAG_GATHER_SELECTED
                 side[1].record(stream)
                 side[1].wait(side[0])
-                _launch(pf, table, ws, info, side[0], pf.phases)
-            fill(js, ws.data_ptr() + int(info.index_offset), int(info.index_row_stride), stream)
-            _launch(p, table, ws, info, stream, p.phases)
-            if side is not None:  # `stream` continues only after the side copy
-                side[2].record(side[0])
-                side[2].wait(stream)
+            try:
+                if side is not None:
+                    _launch(pf, table, ws, info, side[0], pf.phases)
+                fill(js, ws.data_ptr() + int(info.index_offset), int(info.index_row_stride),
+                     stream)
+                _launch(p, table, ws, info, stream, p.phases)
+            finally:
+                if side is not None:  # `stream` continues only after the side copy, on every
+                    side[2].record(side[0])  # exit path (outputs and workspace are freed on it)
+                    side[2].wait(stream)
             del keep
         for j, ko, vo in zip(js, kos, vos):
             out_list[j.layer_idx] = (ko, vo)
@@ -656,6 +705,12 @@ def memoized(fn):
 
     @functools.wraps(fn)
     def wrapper(past_key_values, *args, **kwargs):
+        out = _memo_call(past_key_values, *args, **kwargs)
+        if check_status:
+            raise_on_status()
+        return out
+
+    def _memo_call(past_key_values, *args, **kwargs):
         global _recording
         hm = host_module()
         if hm is None or _timer is not None or _recording is not None:

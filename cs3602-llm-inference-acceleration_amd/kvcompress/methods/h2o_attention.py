@@ -78,6 +78,7 @@ class H2OAttentionManager:
     def _threads(self):
         return self.reduction_threads or CO.threads()
 
+    @E.status_checked
     def update_attention_scores(self, attentions, skip_layers: List[int] = []):
         """h2o_attention.py:84-153 for every given layer in one engine launch per
         (device, dtype, B, H, carried dtype) group: acc <- acc*decay (zero-extended to the new key
@@ -95,6 +96,9 @@ class H2OAttentionManager:
             _check_gpu(attn, f"attention of layer {layer_idx}")
             if attn.stride(3) != 1 or attn.data_ptr() % attn.element_size():
                 attn = attn.contiguous()
+            # the q-sum's thread chunks follow the attention the reference sums (:116), before
+            # any broadcast below
+            chunk = CO.attn_sum_chunk(attn, threads)
             acc = self.accumulated_attention.get(layer_idx)
             old = None
             if acc is not None and acc.size(-1) <= key_len:  # decay (and zero-extend) (:124-146)
@@ -103,15 +107,25 @@ class H2OAttentionManager:
                     raise RuntimeError(
                         f"layer {layer_idx}: accumulated attention on {acc.device}, new attention "
                         f"on {attn.device}: expected all tensors to be on the same device")
-                if acc.shape[:2] != attn.shape[:2]:  # torch.cat raises; + would broadcast
-                    raise RuntimeError(
-                        f"layer {layer_idx}: accumulated attention {tuple(acc.shape)} and new "
-                        f"attention {tuple(attn.shape)} differ in batch / heads (not supported)")
+                if acc.shape[:2] != attn.shape[:2]:
+                    if acc.size(-1) != key_len:  # torch.cat of differing batch / heads (:135)
+                        raise RuntimeError(
+                            f"layer {layer_idx}: Sizes of tensors must match except in dimension "
+                            f"2 (accumulated attention {tuple(acc.shape)}, zero padding "
+                            f"{(b, h, key_len - acc.size(-1))})")
+                    # equal lengths: `acc * decay + attn.sum(dim=2)` (:146-151) broadcasts --
+                    # every element's arithmetic is the same as without the broadcast
+                    try:
+                        shp = torch.broadcast_shapes(tuple(acc.shape), (b, h, key_len))
+                    except RuntimeError as e:
+                        raise RuntimeError(f"layer {layer_idx}: {e}") from None
+                    b, h = shp[0], shp[1]
+                    acc = acc.expand(b, h, key_len)
+                    attn = attn.expand(b, h, q, key_len)
                 old = acc.contiguous()
             # acc.size(-1) > key_len: reset to zeros (:138-144) -- old stays None
             key = (attn.get_device(), attn.dtype, b, h, attn.dtype if old is None else old.dtype)
-            groups.setdefault(key, []).append(
-                (layer_idx, attn, old, CO.attn_sum_chunk(attn, threads)))
+            groups.setdefault(key, []).append((layer_idx, attn, old, chunk))
             self.current_seq_len = key_len
         for (device, dtype, b, h, odt), jobs in groups.items():
             with torch.cuda.device(device):
@@ -141,6 +155,7 @@ class H2OAttentionManager:
             return None
         return acc, m0, m1 - m0, min(self.heavy_hitter_size, m1 - m0)
 
+    @E.status_checked
     def get_heavy_hitter_indices(self, layer_idx: int, seq_len: int) -> torch.Tensor:
         """h2o_attention.py:156-213: ascending middle-local indices of the heavy hitters ([k], or
         [B, k] for batch > 1), computed by the engine."""
@@ -202,6 +217,7 @@ def _run_hh(mgr, rows, out_ptr, out_stride, stream):
     N.check(rc, "kvc_heavy_hitters")
 
 
+@E.status_checked
 def h2o_attention_compress(past_key_values, attention_scores: Optional[Tuple] = None,
                            h2o_manager: Optional[H2OAttentionManager] = None,
                            start_size: int = 4, heavy_hitter_size: int = 64,

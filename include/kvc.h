@@ -79,8 +79,8 @@ enum kvc_flag {
   KVC_FLAG_GATHER_SELECTED = 8      /* GATHER copies only the selected rows.  With the previous
                                        flag: one call's copy in two launches, e.g. the fixed rows
                                        on a second stream while the selection runs.  At most one
-                                       of the two; either implies SELECT and GATHER as two
-                                       kernels (as KVC_FLAG_SPLIT_SELECT_GATHER)               */
+                                       of the two, and only with external_index (the parts
+                                       read the caller's indices; KVC_E_ARG otherwise)         */
 };
 /* Bits the kernels OR into *params.device_status (when not NULL).  The word is sticky: the
  * library never clears it; the caller zeroes it and reads it after the stream has drained. */

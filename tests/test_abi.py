@@ -183,10 +183,14 @@ def test_plan_rejects_unknown_flags():
     assert N.plan(_params(flags=N.FLAG_SPLIT_SELECT_GATHER), table.copy())[0] == 0
     assert N.plan(_params(flags=16), table.copy())[0] == -1
     assert N.plan(_params(flags=1 << 30), table.copy())[0] == -1
-    # the gather-part flags: one at a time
-    assert N.plan(_params(flags=N.FLAG_GATHER_FIXED), table.copy())[0] == 0
-    assert N.plan(_params(flags=N.FLAG_GATHER_SELECTED), table.copy())[0] == 0
-    assert N.plan(_params(flags=N.FLAG_GATHER_FIXED | N.FLAG_GATHER_SELECTED),
+    # the gather-part flags: one at a time, and only over external indices (two launches of
+    # the engine's own selection would SCORE / SELECT into one workspace concurrently)
+    ext = dict(external_index=1, phases=N.PHASE_GATHER)
+    assert N.plan(_params(flags=N.FLAG_GATHER_FIXED, **ext), table.copy())[0] == 0
+    assert N.plan(_params(flags=N.FLAG_GATHER_SELECTED, **ext), table.copy())[0] == 0
+    assert N.plan(_params(flags=N.FLAG_GATHER_FIXED), table.copy())[0] == -1
+    assert N.plan(_params(flags=N.FLAG_GATHER_SELECTED), table.copy())[0] == -1
+    assert N.plan(_params(flags=N.FLAG_GATHER_FIXED | N.FLAG_GATHER_SELECTED, **ext),
                   table.copy())[0] == -1
     assert N.plan(_params(reserved=1), table.copy())[0] == -1
     assert N.plan(_params(flags=N.FLAG_SHARED_INDEX), table.copy())[0] == -1

@@ -79,3 +79,40 @@ def test_select_bounds_reported_and_row_left_unwritten(phases, dt):
     for cap in (0, 100, 8256):
         assert N.debug_select_capacity(p, t, ws.data_ptr(), int(info.workspace_bytes), cap,
                                        stream) == KVC_E_ARG
+
+
+def test_opt_in_status_check_raises_naming_the_bit():
+    """kvcompress._engine.set_status_check(True) (or KVC_CHECK_STATUS=1 at import): a compress
+    call after which the engine's device word is non-zero raises RuntimeError naming the bit and
+    clears the word; clean calls pass.  The bit is set through kvc_debug_select_capacity on the
+    engine's own word, as a dispatch bug inside a call would set it."""
+    from kvcompress import _engine as E
+    from kvcompress.methods import fix_size_l2_compress
+    H, D, n_sel, S = 4, 64, 100, 3000
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(9)
+    k = torch.randn(1, H, S, D, device=dev, generator=g).to(torch.bfloat16)
+    v = torch.randn(1, H, S, D, device=dev, generator=g).to(torch.bfloat16)
+    ko, vo = torch.empty(1, H, n_sel, D, device=dev, dtype=k.dtype), torch.empty(
+        1, H, n_sel, D, device=dev, dtype=k.dtype)
+    t = _table([(k, v, ko, vo, S, n_sel)], H, D)
+    word = E.status_word(0)
+    p = N.Params(dtype=N.KVC_BF16, batch=1, heads=H, head_dim=D, order=N.KVC_ASC,
+                 algo=N.KVC_ALGO_SORT, phases=N.PHASE_SELECT | N.PHASE_GATHER, external_index=0,
+                 flags=0, device_status=word.data_ptr())
+    rc, info = N.plan(p, t)
+    assert rc == 0
+    ws = torch.zeros(int(info.workspace_bytes), dtype=torch.uint8, device=dev)
+    prev = E.set_status_check(True)
+    try:
+        layers = [(k, v)]
+        out = fix_size_l2_compress(layers, fix_kv_size=512, skip_layers=[])  # clean: no raise
+        assert out[0][0].shape[2] == 512
+        assert N.debug_select_capacity(p, t, ws.data_ptr(), int(info.workspace_bytes), 1024,
+                                       torch.cuda.current_stream().cuda_stream) == 0
+        with pytest.raises(RuntimeError, match="KVC_DEV_SELECT_BOUNDS"):
+            fix_size_l2_compress(layers, fix_kv_size=512, skip_layers=[])
+        assert E.device_status(0) == 0  # cleared by the raise
+        fix_size_l2_compress(layers, fix_kv_size=512, skip_layers=[])
+    finally:
+        E.set_status_check(prev)

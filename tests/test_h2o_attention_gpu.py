@@ -351,3 +351,74 @@ def test_fixed_rows_copied_beside_the_selection_match():
         for li in range(L):
             for x, y in zip(outs[li], ref[li]):
                 assert np.array_equal(to_np(x).view(np.uint8), to_np(y).view(np.uint8)), li
+
+
+@pytest.mark.parametrize("dt", ["fp32", "bf16"])
+def test_equal_length_accumulation_broadcasts_batch_and_heads(dt):
+    """`acc * decay + attn.sum(dim=2)` with equal key lengths broadcasts a batch-1 (or head-1)
+    accumulation against the new attention and vice versa (h2o_attention.py:146-151), while the
+    zero-extension's torch.cat (:135) raises: checked against torch's CPU ops."""
+    from kvcompress.methods.h2o_attention import H2OAttentionManager
+    rng = np.random.default_rng(5)
+    tdt = TORCH_DT[dt]
+    for first, second in [((1, 8, 3, 500), (2, 8, 1, 500)), ((2, 8, 3, 500), (1, 8, 2, 500)),
+                          ((1, 1, 2, 300), (2, 4, 1, 300))]:
+        mgr = H2OAttentionManager(start_size=4, heavy_hitter_size=16, recent_size=40)
+        mgr.reduction_threads = torch.get_num_threads()
+        a1 = _tie_attention(rng, first).to(tdt)
+        a2 = _tie_attention(rng, second).to(tdt)
+        mgr.update_attention_scores((a1.to("cuda:0"),))
+        mgr.update_attention_scores((a2.to("cuda:0"),))
+        ref = (torch.zeros(first[:2] + first[3:], dtype=tdt) + a1.sum(dim=2)) * 0.9 + a2.sum(dim=2)
+        got = mgr.accumulated_attention[0]
+        assert got.shape == ref.shape, (first, second)
+        assert np.array_equal(to_np(got).view(np.uint8), to_np(ref).view(np.uint8)), (first, second)
+    mgr = H2OAttentionManager()
+    mgr.update_attention_scores((_tie_attention(rng, (1, 8, 1, 500)).to(tdt).to("cuda:0"),))
+    with pytest.raises(RuntimeError):  # extension: torch.cat of [1,8,*] and zeros [2,8,*]
+        mgr.update_attention_scores((_tie_attention(rng, (2, 8, 1, 501)).to(tdt).to("cuda:0"),))
+
+
+LONG = json.load(open(os.path.join(HERE, "golden", "h2o_attention_long.json")))
+
+
+@pytest.mark.parametrize("dt", ["bf16", "fp32"])
+@pytest.mark.parametrize("native", [True, False])
+def test_long_context_steps_match_reference_golden(dt, native):
+    """BASELINE cfg4's geometry against the unmodified reference (tests/golden/
+    h2o_attention_long.json): S = 16 384, start 4 / heavy 64 / recent 444, three q = 1 steps.  The
+    middle (15 936) is >= OVERLAP_MIN_ZONE, so the sink / recent rows are copied on a side stream
+    beside the heavy-hitter selection; with native=True the third step is replayed by
+    kvc_host.run_h2o (its fork / join), with native=False every step takes the Python path
+    (execute_shared's fork / join).  Accumulations, heavy hitters and K / V are all checked."""
+    from gen_h2o_attention_long import att_seed as l_att, kv_seed as l_kv
+    from kvcompress.methods import h2o_attention as HA
+    H, D, S, L = LONG["H"], LONG["D"], LONG["S"], LONG["layers"]
+    assert S - LONG["kw"]["start_size"] - LONG["kw"]["recent_size"] >= HA.OVERLAP_MIN_ZONE
+    kv = [(to_dev(prng.gen_keys(l_kv(li), (1, H, S, D), dt)),
+           to_dev(prng.gen_values(l_kv(li), (1, H, S, D), dt))) for li in range(L)]
+    mgr = HA.H2OAttentionManager(decay_factor=LONG["decay"], num_layers=L, num_heads=H,
+                                 **LONG["kw"])
+    mgr.reduction_threads = LONG["threads"]
+    HA.step_memo.clear()
+    r0 = HA.step_stats["replayed"]
+    HA.replay_steps = native
+    try:
+        for st in range(LONG["steps"]):
+            atts = tuple(to_dev(h2o_inputs.attention(l_att(st, li), H, 1, S, dt))
+                         for li in range(L))
+            out = HA.h2o_attention_compress(list(kv), attention_scores=atts, h2o_manager=mgr,
+                                            skip_layers=[], **LONG["kw"])
+            rec = LONG["results"][dt][st]
+            for li in range(L):
+                assert out[li][0].shape[2] == rec["n_out"][li], (st, li)
+                assert sha(to_np(out[li][0])) == rec["k"][li], ("K", st, li)
+                assert sha(to_np(out[li][1])) == rec["v"][li], ("V", st, li)
+                assert sha(to_np(mgr.accumulated_attention[li])) == rec["acc"][li], ("acc", st, li)
+                assert mgr.get_heavy_hitter_indices(li, S).cpu().tolist() == rec["idx"][li], \
+                    ("idx", st, li)
+    finally:
+        HA.replay_steps = True
+    assert (HA.step_stats["replayed"] - r0 >= 1) == native
+    from kvcompress import _engine
+    assert _engine.device_status(0) == 0

@@ -234,3 +234,38 @@ def test_oracle_replays_mixed_dtype_goldens(si):
             if out is not None:
                 assert sha(out[li][0]) == rec["k"][li] and sha(out[li][1]) == rec["v"][li], (st, li)
     replay_mixed(gold, si, mgr, compress, check)
+
+
+def test_oracle_replays_long_context_golden():
+    """BASELINE cfg4's geometry (tests/golden/h2o_attention_long.json, S = 16 384, middle 15 936,
+    three q = 1 steps, bf16 and fp32): the oracle reproduces the unmodified reference's
+    accumulations, heavy hitters and compressed K / V; the boundary is tied in most steps."""
+    from gen_h2o_attention_long import att_seed as l_att, kv_seed as l_kv
+    with open(os.path.join(GOLD, "h2o_attention_long.json")) as f:
+        gold = json.load(f)
+    H, D, S, L = gold["H"], gold["D"], gold["S"], gold["layers"]
+    tied = total = 0
+    for dt in ("bf16", "fp32"):
+        kv = [(prng.gen_keys(l_kv(li), (1, H, S, D), dt), prng.gen_values(l_kv(li), (1, H, S, D), dt))
+              for li in range(L)]
+        mgr = HO.H2OManager(decay_factor=gold["decay"], threads=gold["threads"],
+                            capability=gold["capability"], **gold["kw"])
+        for st in range(gold["steps"]):
+            atts = tuple(h2o_inputs.attention(l_att(st, li), H, 1, S, dt) for li in range(L))
+            out = HO.h2o_attention_compress(list(kv), attention_scores=atts, h2o_manager=mgr,
+                                            skip_layers=[], **gold["kw"])
+            rec = gold["results"][dt][st]
+            for li in range(L):
+                assert sha(mgr.acc[li]) == rec["acc"][li], (dt, st, li)
+                idx = mgr.get_heavy_hitter_indices(li, S)
+                assert idx.tolist() == rec["idx"][li], (dt, st, li)
+                assert sha(out[li][0]) == rec["k"][li] and sha(out[li][1]) == rec["v"][li], \
+                    (dt, st, li)
+                m0, m1 = mgr.start_size, S - mgr.recent_size
+                agg = HO.to_f32(HO.head_sum(mgr.acc[li][:, :, m0:m1], gold["threads"],
+                                            gold["capability"]))[0]
+                kept = np.zeros(m1 - m0, bool)
+                kept[idx] = True
+                total += 1
+                tied += bool(np.intersect1d(agg[kept], agg[~kept]).size)
+    assert tied >= total // 2, (tied, total)

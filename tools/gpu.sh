@@ -14,8 +14,12 @@
 #              the first and last rank) + a rocprofv3 trace of the last rank's cfg5 pyramid step
 #                                                                               -> shard.jsonl, shardprof/
 #   dtypes     the headline in fp32 and fp16 K/V                                -> dtypes.jsonl
-#   ab         A/B of library builds named in $AB_LIBS (files in kvcompress/_lib) on the
-#              workloads in $AB_WORKLOADS (bench.py, 2 repeats)                   -> ab.jsonl
+#   ab:NAME    the A/B recipe NAME of tools/ab_recipes.txt: library variants (built beforehand by
+#              tools/build_variant.sh from tools/ab_variants.txt) on bench.py workloads, each
+#              line tagged with the recipe                                        -> ab.jsonl
+#   h2olong    rocprofv3 kernel stats of the long h2o_attention call
+#              (tools/h2o_long_profile.py)                                        -> h2oprof/
+#   heap       tools/heap_probe (register heap select vs std::partial_sort)      -> heap_probe.jsonl
 # Every GPU step runs under its own time limit and the first failure ends the call.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"
@@ -82,25 +86,45 @@ for step in "$@"; do
     pmc)
       bash tools/pmc_round.sh > "$O/pmc_round.out" 2>&1 || { tail -20 "$O/pmc_round.out"; exit 1; }
       tail -c 3000 "$O/pmc_round.out" ;;
-    ab)
-      : > "$O/ab.jsonl"
-      for rep in ${AB_REPS:-1 2}; do
-        for lib in ${AB_LIBS:?}; do
-          for w in ${AB_WORKLOADS:-fix512-s16384}; do
-            KVC_LIB="$LIBDIR/$lib" timeout -k 10 200 python bench.py --workload $w --steps 20 \
-                --warmup 5 --no-cpu-baseline $AB_ARGS > "$O/ab_one.json" 2> "$O/ab.err" || { tail "$O/ab.err"; exit 1; }
-            echo "{\"rep\": $rep, \"lib\": \"$lib\", \"workload\": \"$w\", \"args\": \"$AB_ARGS\", \"r\": $(cat "$O/ab_one.json")}" >> "$O/ab.jsonl"
+    ab:*)
+      name="${step#ab:}"
+      line=$(grep -E "^$name[[:space:]]" tools/ab_recipes.txt) || { echo "recipe $name not in tools/ab_recipes.txt"; exit 2; }
+      libs=""; wls="fix512-s16384"; reps="1 2"; args=""; test=""
+      for f in $line; do
+        case "$f" in
+          libs=*) libs="${f#libs=}" ;;
+          workloads=*) wls="${f#workloads=}" ;;
+          reps=*) reps=$(seq 1 "${f#reps=}") ;;
+          args=*) args="${f#args=}"; args="${args//+/ }" ;;
+          test=*) test="${f#test=}" ;;
+        esac
+      done
+      if [ -n "$test" ]; then
+        last="${libs##*,}"
+        KVC_LIB="$LIBDIR/$last.so" timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py \
+            tests/test_gpu_fuzz.py -m gpu -x -q --timeout 120 --timeout-method thread \
+            -p no:cacheprovider > "$O/ab_pytest.log" 2>&1 || { tail -30 "$O/ab_pytest.log"; exit 1; }
+        tail -1 "$O/ab_pytest.log"
+      fi
+      for rep in $reps; do
+        for lib in ${libs//,/ }; do
+          for w in ${wls//,/ }; do
+            KVC_LIB="$LIBDIR/$lib.so" timeout -k 10 200 python bench.py --workload $w --steps 20 \
+                --warmup 5 --no-cpu-baseline $args > "$O/ab_one.json" 2> "$O/ab.err" || { tail "$O/ab.err"; exit 1; }
+            echo "{\"recipe\": \"$name\", \"rep\": $rep, \"lib\": \"$lib\", \"workload\": \"$w\", \"args\": \"$args\", \"r\": $(cat "$O/ab_one.json")}" >> "$O/ab.jsonl"
           done
         done
       done
-      python3 - "$O/ab.jsonl" <<'EOF'
-import json, sys
-for l in open(sys.argv[1]):
-    d = json.loads(l); r = d["r"]
-    print(d["rep"], d["lib"], d["workload"], round(r["ms_per_step"], 4),
-          {k: round(v, 4) for k, v in r["kernel_ms_per_step"].items()})
-EOF
-      ;;
+      python3 tools/ab_summary.py "$O/ab.jsonl" "$name" ;;
+    h2olong)
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats \
+          --output-format csv -d "$O/h2oprof" -o run -- python3 "$R/tools/h2o_long_profile.py" \
+          > "$O/h2oprof.log" 2>&1 ) || { tail "$O/h2oprof.log"; exit 1; }
+      grep ms_per_call "$O/h2oprof.log"
+      python3 tools/ab_summary.py --kernel-stats "$O/h2oprof/run_kernel_stats.csv" ;;
+    heap)
+      timeout -k 10 120 tools/heap_probe > "$O/heap_probe.jsonl" 2>&1 || { cat "$O/heap_probe.jsonl"; exit 1; }
+      cat "$O/heap_probe.jsonl" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
