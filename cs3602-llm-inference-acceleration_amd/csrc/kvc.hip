@@ -63,6 +63,32 @@ constexpr int kBig = 0x7FFFFFFF;
 // (chunks of kArgLayers, 8.7 KiB): no host->device table copy, whose completion would stand
 // ~10 us between the copy and the first kernel of every call.
 constexpr int kArgLayers = 64;
+// SELECT_GATHER launches of at most this many rows (fewer than the 256 CUs: one row per CU)
+// copy each row's sink / tail rows in a second workgroup beside the selecting one
+#ifndef KVC_SPLIT_COPY_ROWS
+#define KVC_SPLIT_COPY_ROWS 255
+#endif
+constexpr int kSplitCopyRows = KVC_SPLIT_COPY_ROWS;
+// SELECT_GATHER's output stores: non-temporal (written once) unless built with KVC_SG_NTS=false
+#ifndef KVC_SG_NTS
+#define KVC_SG_NTS true
+#endif
+constexpr bool kSgNts = KVC_SG_NTS;
+// the fused copy's row loads: default policy unless built with KVC_SG_NTL=true (non-temporal)
+#ifndef KVC_SG_NTL
+#define KVC_SG_NTL false
+#endif
+constexpr bool kSgNtl = KVC_SG_NTL;
+// the wave chain's segments of <= 64 positions in registers (wave_tiny_chain); 0: LDS levels
+#ifndef KVC_TINY_CHAIN
+#define KVC_TINY_CHAIN 1
+#endif
+constexpr bool kTinyChain = KVC_TINY_CHAIN;
+// partition_level loads s_m with g_{m+1} (single-window levels); 0: after the swaps
+#ifndef KVC_EARLY_CUT
+#define KVC_EARLY_CUT 1
+#endif
+constexpr bool kEarlyCut = KVC_EARLY_CUT;
 struct LayerChunk {
   kvc_layer_t l[kArgLayers];
 };
@@ -1178,6 +1204,123 @@ __device__ __forceinline__ void p2_window0(const KeyT* key, uint16_t* spos, uint
   }
 }
 
+// The chain's last levels, once the segment [lo, hi) holds at most 64 positions, run by one wave
+// with the segment in registers: lane i holds position lo + i (key, index).  A level is the same
+// libstdc++ step as partition_level (std::__move_median_to_first + std::__unguarded_partition:
+// g_t <-> s_t for the prefix t <= m with g_t < s_t, cut = min(g_{m+1}, s_m)), computed from two
+// ballots: the g / s rank -> lane tables are built by forward permutes (ds_permute) and each
+// swapped lane fetches its partner's entry by a backward permute -- no LDS memory round trips,
+// no rank-table stores.  The final stable insertion sort ranks the segment's lanes against each
+// other, and every lane writes its entry back once.  depth == 0 (the introsort / introselect
+// depth limit) writes the registers back and takes the serial heap path, as run_chain does.
+// Returns with the segment's final arrangement in key / idx (only the first-k SET matters).
+template <typename KeyT>
+__device__ __forceinline__ void wave_tiny_chain(KeyT* key, uint16_t* idx, int k, bool topk,
+                                                int thr, int lo, int hi, int depth) {
+  const int lane = threadIdx.x & 63;
+  const int m = hi - lo;  // <= 64
+  const bool own = lane < m;
+  uint32_t kk = own ? (uint32_t)key[lo + lane] : 0xFFFFFFFFu;
+  uint32_t ii = own ? (uint32_t)idx[lo + lane] : 0u;
+  int slo = 0, shi = m;          // the segment, relative to lo
+  const int kr = k - lo;         // k relative to lo
+  int dest = lane;               // where this lane's entry is written back
+  bool heap = false;
+  while (true) {
+    if (slo == kr || shi == kr) break;  // a partition boundary sits at k
+    if (shi - slo <= thr) {  // final stable insertion sort: rank within [slo, shi)
+      const bool in = lane >= slo && lane < shi;
+      int r = 0;
+      for (int j = slo; j < shi; ++j) {  // uniform trip count
+        const uint32_t kj = (uint32_t)__builtin_amdgcn_readlane((int)kk, j);
+        r += (kj < kk || (kj == kk && j < lane)) ? 1 : 0;
+      }
+      dest = in ? slo + r : lane;
+      break;
+    }
+    if (depth == 0) {  // depth limit: the serial heap algorithms on LDS
+      heap = true;
+      break;
+    }
+    --depth;
+    // std::__move_median_to_first(slo, slo + 1, mid, shi - 1)
+    const int a = slo + 1, b = slo + (shi - slo) / 2, c = shi - 1;
+    const uint32_t ka = (uint32_t)__builtin_amdgcn_readlane((int)kk, a);
+    const uint32_t kb = (uint32_t)__builtin_amdgcn_readlane((int)kk, b);
+    const uint32_t kc = (uint32_t)__builtin_amdgcn_readlane((int)kk, c);
+    int ch;
+    if (ka < kb) {
+      if (kb < kc) ch = b; else if (ka < kc) ch = c; else ch = a;
+    } else if (ka < kc) {
+      ch = a;
+    } else if (kb < kc) {
+      ch = c;
+    } else {
+      ch = b;
+    }
+    const uint32_t p = ch == a ? ka : ch == b ? kb : kc;
+    const uint32_t klo = (uint32_t)__builtin_amdgcn_readlane((int)kk, slo);
+    const uint32_t ich = (uint32_t)__builtin_amdgcn_readlane((int)ii, ch);
+    const uint32_t ilo = (uint32_t)__builtin_amdgcn_readlane((int)ii, slo);
+    kk = lane == slo ? p : lane == ch ? klo : kk;
+    ii = lane == slo ? ich : lane == ch ? ilo : ii;
+    // std::__unguarded_partition(slo + 1, shi, pivot = slo)
+    const bool inr = lane > slo && lane < shi;
+    const bool ge = inr && kk >= p, le = inr && kk <= p;
+    const uint64_t GE = __builtin_amdgcn_ballot_w64(ge), LE = __builtin_amdgcn_ballot_w64(le);
+    const int tot_le = __popcll(LE);
+    const int A = mbcnt(GE, 0);                    // ge lanes below
+    const int lin = mbcnt(LE, 0) + (le ? 1 : 0);   // le lanes in (slo, lane]
+    const bool sg = ge && A + lin < tot_le;        // g_t (t = A + 1) with g_t < s_t: swapped
+    const uint64_t SG = __builtin_amdgcn_ballot_w64(sg);
+    const int msw = __popcll(SG);
+    const int srk = tot_le - lin + 1;              // s rank of an le lane
+    const bool ss = le && srk <= msw;              // s_t, t <= m: swapped
+    // rank -> lane tables: lane t - 1 of gt / st receives g_t / s_t (others write lane 63,
+    // never read: m <= 31)
+    const int gt = __builtin_amdgcn_ds_permute((sg ? A : 63) * 4, lane);
+    const int st = __builtin_amdgcn_ds_permute((ss ? srk - 1 : 63) * 4, lane);
+    const int tab = gt | (st << 8);
+    const int t1 = sg ? A : ss ? srk - 1 : 0;      // this lane's rank - 1
+    const int pt = __builtin_amdgcn_ds_bpermute(t1 * 4, tab);
+    const int partner = sg ? (pt >> 8) : ss ? (pt & 0xFF) : lane;
+    if constexpr (sizeof(KeyT) == 2) {
+      const uint32_t w = __builtin_amdgcn_ds_bpermute(partner * 4, (int)(kk << 16 | ii));
+      kk = w >> 16;
+      ii = w & 0xFFFFu;
+    } else {
+      const uint32_t nk = __builtin_amdgcn_ds_bpermute(partner * 4, (int)kk);
+      ii = __builtin_amdgcn_ds_bpermute(partner * 4, (int)ii);
+      kk = nk;
+    }
+    // cut = min(g_{m+1}, s_m): the first unswapped ge lane, the lowest swapped le lane
+    const uint64_t GN = GE & ~SG;
+    const int gnext = GN ? (int)__builtin_ctzll(GN) : kBig;
+    const uint64_t SS = __builtin_amdgcn_ballot_w64(ss);
+    const int cut = min(gnext, SS ? (int)__builtin_ctzll(SS) : kBig);
+    const bool right = topk ? cut <= kr - 1 : kr > cut;
+    slo = right ? cut : slo;
+    shi = right ? shi : cut;
+  }
+  if (own) {
+    key[lo + dest] = (KeyT)kk;
+    idx[lo + dest] = (uint16_t)ii;
+  }
+  if (heap) {
+    wave_sync();
+    if (lane == 0) {
+      if (topk) {
+        heap_select(key + lo + slo, idx + lo + slo, kr - slo, shi - slo);
+        kv_swap(key, idx, lo + slo, k - 1);
+      } else {
+        make_heap(key + lo + slo, idx + lo + slo, shi - slo);
+        sort_heap(key + lo + slo, idx + lo + slo, shi - slo);
+      }
+    }
+  }
+  wave_sync();
+}
+
 // One partition level over [lo, hi) with at most JM positions per lane (compile-time bound; the
 // passes stop at the segment's own J with a scalar branch).  Returns cut.  See run_chain for
 // the algorithm.  P1 and P2 are issue-bound at the long levels (16 waves of 16 rows of 64
@@ -1298,6 +1441,9 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
   }
   // g_{m+1}, the first unswapped ge position (none when every ge position is swapped)
   int gnext = msw >= tot_ge ? kBig : msw < cap ? uni((int)gpos[msw + 1]) : kBig;
+  // s_m of a single-window level (msw <= cap: P4 never rewrites the tables), loaded beside
+  // g_{m+1} instead of after the swaps' barrier
+  const int s_m = kEarlyCut && msw > 0 && msw <= cap ? uni((int)spos[msw]) : kBig;
   KVC_TICK(t2);
   // ---- m >= cap (rare): the level's flags, from the keys before any swap (the median slot is
   // physical now), kept in registers for the later windows' scatters (the swapped pairs are
@@ -1429,6 +1575,7 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
     }
   }
 #endif
+  if (kEarlyCut && msw <= cap) return min(gnext, s_m);
   return min(gnext, msw > 0 ? uni((int)spos[msw - wb]) : kBig);
 }
 
@@ -1455,6 +1602,12 @@ __device__ __forceinline__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spo
   const int tid = (NT == 64) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   while (true) {
     if (lo == k || hi == k) return 0;  // a partition boundary sits at k: the set is final
+    if constexpr (NT == 64 && kTinyChain) {
+      if (hi - lo <= 64 && hi - lo > thr) {  // the last levels from registers
+        wave_tiny_chain(key, idx, k, topk, thr, lo, hi, depth);
+        return 0;
+      }
+    }
     if (hi - lo <= thr) {              // final (stable) insertion sort of the segment
       if (tid < 64) wave_stable_sort(key, idx, lo, hi);
       group_sync<NT>();
@@ -2312,9 +2465,11 @@ __host__ __device__ __forceinline__ bool layer_selects(const kvc_layer_t& y) {
 // Thread tid copies 16-B chunk tid % NC of output tokens tid / NC + i * (NT / NC): the same
 // coalesced units as a flat unit loop (consecutive threads, consecutive 16-B units) with the
 // chunk and its address offsets fixed per thread; the last NT % NC threads idle.
+// part: PART_ALL, or PART_SELECTED / PART_FIXED (the row's copy split between the selecting
+// workgroup and a copy-only one, part_rows / part_row).
 template <int DT, int NC, int NT = kSelThreads, bool NTS = false>
 __device__ __forceinline__ void gather_row(const kvc_layer_t* __restrict__ ly, int r, int H,
-                                           const uint16_t* sel) {
+                                           const uint16_t* sel, int part = PART_ALL) {
   constexpr int ESZ = DTypeTraits<DT>::esz;
   constexpr int BATCH = 4;
   constexpr int TPI = NT / NC;  // tokens per pass
@@ -2324,6 +2479,7 @@ __device__ __forceinline__ void gather_row(const kvc_layer_t* __restrict__ ly, i
   const int n_out = ly->n_out;
   const int b = r / H, h = r - (r / H) * H;
   const int sink = ly->sink_len, nsel = ly->n_select;
+  const int nv = part_rows(*ly, part);  // rows this workgroup copies
   const char* kb = static_cast<const char*>(ly->k) +
                    ((int64_t)b * ly->k_stride[0] + (int64_t)h * ly->k_stride[1]) * ESZ + c * 16;
   const char* vb = static_cast<const char*>(ly->v) +
@@ -2331,14 +2487,15 @@ __device__ __forceinline__ void gather_row(const kvc_layer_t* __restrict__ ly, i
   const int64_t kss = ly->k_stride[2] * ESZ, vss = ly->v_stride[2] * ESZ;
   char* ko = static_cast<char*>(ly->k_out) + (int64_t)r * n_out * NC * 16 + c * 16;
   char* vo = static_cast<char*>(ly->v_out) + (int64_t)r * n_out * NC * 16 + c * 16;
-  for (int tb = tq; tb < n_out; tb += TPI * BATCH) {
+  for (int tb = tq; tb < nv; tb += TPI * BATCH) {
     uint4 xk[BATCH], xv[BATCH];
     bool gat[BATCH];
 #pragma unroll
     for (int i = 0; i < BATCH; ++i) {
-      const int t = tb + i * TPI;
+      const int v = tb + i * TPI;
+      const int t = part_row(v, sink, nsel, part);
       gat[i] = false;
-      if (t < n_out) {
+      if (v < nv) {
         int src;
         if (t < sink) {
           src = t;
@@ -2350,14 +2507,23 @@ __device__ __forceinline__ void gather_row(const kvc_layer_t* __restrict__ ly, i
         } else {
           src = ly->tail_start + (t - sink - nsel);
         }
-        xk[i] = *reinterpret_cast<const uint4*>(kb + src * kss);
-        xv[i] = *reinterpret_cast<const uint4*>(vb + src * vss);
+        if constexpr (kSgNtl) {  // kept rows are read once: non-temporal
+          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+          const u32x4 a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(kb + src * kss));
+          const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(vb + src * vss));
+          xk[i] = make_uint4(a.x, a.y, a.z, a.w);
+          xv[i] = make_uint4(q.x, q.y, q.z, q.w);
+        } else {
+          xk[i] = *reinterpret_cast<const uint4*>(kb + src * kss);
+          xv[i] = *reinterpret_cast<const uint4*>(vb + src * vss);
+        }
       }
     }
 #pragma unroll
     for (int i = 0; i < BATCH; ++i) {
-      const int t = tb + i * TPI;
-      if (t < n_out) {
+      const int v = tb + i * TPI;
+      const int t = part_row(v, sink, nsel, part);
+      if (v < nv) {
         uint4 a = xk[i], q = xv[i];
         if (gat[i]) {
           a = canon_nan_dt<DT>(a);
@@ -2390,15 +2556,27 @@ template <int KC, int NT, int NC>
 __global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT))
     select_gather_kernel(const LayerChunk T, int H, int BH, int dt, int order, int algo,
                          const char* __restrict__ norms, int64_t norm_stride, int wave_seg,
-                         int n_cap, int cap, uint32_t* status) {
+                         int n_cap, int cap, uint32_t* status, int split_rows) {
   typedef typename DTypeTraits<KC>::key_t KeyT;
   constexpr int ESZ = DTypeTraits<KC>::esz;
   constexpr int MAXN = NT == kSelThreads ? kZoneMax : NT * 16;
   __shared__ SelScalars<KeyT> sc;
-  const kvc_layer_t* ly = T.l + blockIdx.x / BH;
-  const int r = (int)(blockIdx.x % BH);
+  // split_rows > 0 (few rows: fewer than the CUs): workgroups [split_rows, 2 split_rows) copy the
+  // sink / tail rows of row blockIdx - split_rows on otherwise idle CUs while the row's own
+  // workgroup selects; the selecting workgroup then copies only the selected rows
+  const bool copier = split_rows > 0 && (int)blockIdx.x >= split_rows;
+  const int wg = copier ? (int)blockIdx.x - split_rows : (int)blockIdx.x;
+  const kvc_layer_t* ly = T.l + wg / BH;
+  const int r = wg % BH;
   if (ly->n_out == 0) return;
   const bool selects = layer_selects(*ly);
+  if (copier) {
+    if (selects)
+      with_dt<KC>(dt, [&](auto D) {
+        gather_row<D.value, NC, NT, kSgNts>(ly, r, H, nullptr, PART_FIXED);
+      });
+    return;
+  }
   const char* nrow = norms + (int64_t)(ly->row0 + r) * norm_stride * ESZ;
   char* arrays;
   if constexpr (NT == kSelThreads) {
@@ -2419,7 +2597,8 @@ __global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT))
     __syncthreads();
   }
   with_dt<KC>(dt, [&](auto D) {
-    gather_row<D.value, NC, NT, true>(ly, r, H, selects ? sel : nullptr);
+    gather_row<D.value, NC, NT, kSgNts>(ly, r, H, selects ? sel : nullptr,
+                                      split_rows > 0 && selects ? PART_SELECTED : PART_ALL);
   });
 }
 
@@ -2921,17 +3100,25 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
                          !long_zone && part == PART_ALL &&
                          !(p->flags & KVC_FLAG_SPLIT_SELECT_GATHER);
     if (fuse_sg) {  // this chunk's gather happens inside the select kernel
-      const dim3 rows_grid((unsigned)(cn * BH));
+      const int rows = cn * BH;
+      const dim3 rows_grid((unsigned)rows);
       const int ks = (int)sizeof(KeyT);
       if (n_cap <= kSmallZone) {
         const int cap = sel_cap(n_cap, ks, kSmallBudget);
         return launch_k(select_gather_kernel<KC, kSelThreadsSmall, NC>, rows_grid,
                         dim3(kSelThreadsSmall), sel_bytes(n_cap, ks, cap), s, T, H, BH, DT,
-                        p->order, p->algo, norms, nstride, kWaveSegSmall, n_cap, cap, status);
+                        p->order, p->algo, norms, nstride, kWaveSegSmall, n_cap, cap, status, 0);
       }
-      return launch_k(select_gather_kernel<KC, kSelThreads, NC>, rows_grid, dim3(kSelThreads), 0,
-                      s, T, H, BH, DT, p->order, p->algo, norms, nstride, kWaveSeg, n_cap, 0,
-                      status);
+      // fewer rows than CUs (e.g. 4 layers per GPU of an 8-way layer split): one row per CU and
+      // idle CUs -- the sink / tail rows get copy-only workgroups of their own
+      bool fixed = false;
+      for (int l = c0; l < c0 + cn; ++l)
+        fixed |= layer_selects(layers[l]) && layers[l].sink_len + layers[l].tail_len > 0;
+      const int split = fixed && rows <= kSplitCopyRows ? rows : 0;
+      return launch_k(select_gather_kernel<KC, kSelThreads, NC>,
+                      dim3((unsigned)(split ? 2 * rows : rows)), dim3(kSelThreads), 0, s, T, H,
+                      BH, DT, p->order, p->algo, norms, nstride, kWaveSeg, n_cap, 0, status,
+                      split);
     }
     char* scratch = w + round_up(info.index_offset + (size_t)info.rows * istride * 4, 256);
     uint64_t* st = stamps ? stamps + (size_t)layers[c0].row0 * 32 : nullptr;
@@ -2979,7 +3166,7 @@ static int debug_select_impl(const kvc_params_t* p, const kvc_layer_t* layers, i
     return with_nc(nc, [&](auto ncv) {
       return launch_k(select_gather_kernel<KC, kSelThreadsSmall, decltype(ncv)::value>, grid,
                       dim3(kSelThreadsSmall), lds, s, T, H, BH, DT, p->order, p->algo, norms,
-                      info.norm_row_stride, kWaveSegSmall, zone_cap, cap, p->device_status);
+                      info.norm_row_stride, kWaveSegSmall, zone_cap, cap, p->device_status, 0);
     });
   });
 }

@@ -10,6 +10,86 @@
 
 #include "kvc_serial.h"
 
+// Lane-by-lane model of wave_tiny_chain's level (csrc/kvc.hip): the segment [lo, hi) of at
+// most 64 positions in "lanes" (lane i = position lo + i); the median move, the ge / le ballots,
+// the g / s ranks from mbcnt counts, the rank -> lane tables of the forward permutes and the
+// partner fetch of the backward permutes, exactly as the kernel computes them.  Returns cut.
+static int tiny_level(uint32_t* K, uint32_t* I, int lo, int hi) {
+  int m = hi - lo;
+  uint32_t kk[64], ii[64];
+  for (int l = 0; l < 64; ++l) {
+    kk[l] = l < m ? K[lo + l] : 0xFFFFFFFFu;
+    ii[l] = l < m ? I[lo + l] : 0u;
+  }
+  const int slo = 0, shi = m;
+  const int a = slo + 1, b = slo + (shi - slo) / 2, c = shi - 1;
+  const uint32_t ka = kk[a], kb = kk[b], kc = kk[c];
+  int ch;
+  if (ka < kb) {
+    if (kb < kc) ch = b; else if (ka < kc) ch = c; else ch = a;
+  } else if (ka < kc) {
+    ch = a;
+  } else if (kb < kc) {
+    ch = c;
+  } else {
+    ch = b;
+  }
+  const uint32_t p = ch == a ? ka : ch == b ? kb : kc;
+  const uint32_t klo = kk[slo], ich = ii[ch], ilo = ii[slo];
+  kk[ch] = klo; kk[slo] = p;
+  ii[ch] = ilo; ii[slo] = ich;
+  uint64_t GE = 0, LE = 0;
+  bool ge[64], le[64];
+  for (int l = 0; l < 64; ++l) {
+    const bool inr = l > slo && l < shi;
+    ge[l] = inr && kk[l] >= p;
+    le[l] = inr && kk[l] <= p;
+    GE |= (uint64_t)ge[l] << l;
+    LE |= (uint64_t)le[l] << l;
+  }
+  const int tot_le = __builtin_popcountll(LE);
+  int A[64], lin[64], srk[64];
+  bool sg[64], ss[64];
+  uint64_t SG = 0;
+  for (int l = 0; l < 64; ++l) {
+    const uint64_t below = l ? (~0ull >> (64 - l)) : 0ull;
+    A[l] = __builtin_popcountll(GE & below);
+    lin[l] = __builtin_popcountll(LE & below) + (le[l] ? 1 : 0);
+    sg[l] = ge[l] && A[l] + lin[l] < tot_le;
+    SG |= (uint64_t)sg[l] << l;
+  }
+  const int msw = __builtin_popcountll(SG);
+  uint64_t SS = 0;
+  int gt[64], st[64];
+  for (int l = 0; l < 64; ++l) gt[l] = st[l] = -1;
+  for (int l = 0; l < 64; ++l) {  // forward permutes (dump lane 63)
+    srk[l] = tot_le - lin[l] + 1;
+    ss[l] = le[l] && srk[l] <= msw;
+    SS |= (uint64_t)ss[l] << l;
+    gt[sg[l] ? A[l] : 63] = l;
+    st[ss[l] ? srk[l] - 1 : 63] = l;
+  }
+  uint32_t nk[64], ni[64];
+  for (int l = 0; l < 64; ++l) {
+    int partner = l;
+    if (sg[l]) partner = st[A[l]];
+    else if (ss[l]) partner = gt[srk[l] - 1];
+    nk[l] = kk[partner];
+    ni[l] = ii[partner];
+  }
+  for (int l = 0; l < m; ++l) {
+    K[lo + l] = nk[l];
+    I[lo + l] = ni[l];
+  }
+  const uint64_t GN = GE & ~SG;
+  const int gnext = GN ? __builtin_ctzll(GN) : 0x7FFFFFFF;
+  const int cut = std::min(gnext, SS ? __builtin_ctzll(SS) : 0x7FFFFFFF);
+  return cut == 0x7FFFFFFF ? cut : lo + cut;
+}
+
+static int g_tiny = 0;  // model_select: segments of 16 < n <= 64 (> thr) through tiny_level
+extern "C" void model_set_tiny(int on) { g_tiny = on; }
+
 extern "C" int model_select(const uint32_t* keys_in, int n, int k, int topk, int32_t* out,
                             int* path) {
   using namespace kvc;
@@ -44,6 +124,15 @@ extern "C" int model_select(const uint32_t* keys_in, int n, int k, int topk, int
           break;
         }
         --depth;
+        if (g_tiny && hi - lo <= 64) {
+          const int cut = tiny_level(K, I, lo, hi);
+          if (topk) {
+            if (cut <= k - 1) lo = cut; else hi = cut;
+          } else {
+            if (k <= cut) hi = cut; else lo = cut;
+          }
+          continue;
+        }
         move_median_to_first(K, I, lo, lo + 1, lo + (hi - lo) / 2, hi - 1);
         const uint32_t p = K[lo];
         std::vector<int> G, S;

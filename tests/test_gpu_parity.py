@@ -485,3 +485,50 @@ def test_mid_length_zones_four_rows_per_cu(dtype, variant, launch_path):
                 b = bits[rk.dtype.itemsize]
                 assert np.array_equal(to_np(ko).view(b), rk.view(b)) and \
                     np.array_equal(to_np(vo).view(b), rv.view(b)), (S, fn.__name__, kw)
+
+
+_SPLIT_CACHE = {}
+
+
+def _split_layers(dt):
+    """Nine [1, 32, 9000, 80] K/V layers (generated once per dtype for the tests below)."""
+    if dt not in _SPLIT_CACHE:
+        shape = (1, 32, 9000, 80)
+        _SPLIT_CACHE.clear()
+        _SPLIT_CACHE[dt] = [(prng.gen_keys(6100 + i, shape, dt, "normal"),
+                             prng.gen_values(6100 + i, shape, dt)) for i in range(9)]
+    return _SPLIT_CACHE[dt]
+
+
+@pytest.mark.parametrize("name,kw", [
+    ("h2o_l2", dict(start_size=4, heavy_hitter_size=64, recent_size=444, skip_layers=[])),
+    ("pyramid_kv", dict(base_size=512, skip_layers=[], num_layers_total=32, layer_offset=28)),
+    ("snapkv_lite", dict(observation_window=32, keep_size=512, skip_layers=[])),
+    ("adaptive_l2", dict(target_size=512, skip_layers=[])),
+])
+@pytest.mark.parametrize("dt", ["bf16", "fp16"])
+def test_few_rows_split_copy_matches_oracle(name, kw, dt):
+    """Calls with fewer selection rows than CUs and zones above the 512-thread path (4 layers x
+    32 heads: one rank's share of an 8-way layer split) copy each row's sink / tail
+    rows in a second workgroup beside the selecting one (select_gather_kernel split_rows); the
+    outputs are bit-identical to the oracle's.  Nine layers (288 rows) take the one-workgroup
+    copy on the same data."""
+    L = 4
+    layers = _split_layers(dt)
+    okw = {k: v for k, v in kw.items() if k not in ("num_layers_total", "layer_offset")}
+    fn = _method(name)
+    for n in (L, 9):
+        if name == "pyramid_kv":  # the last n layers of a 32-layer model (depth-dependent sizes)
+            okw_n = dict(okw, skip_layers=list(range(32 - n)))  # stand-ins, left alone
+            ref = oracle.pyramid_kv_compress([layers[0]] * (32 - n) + layers[:n], **okw_n)[32 - n:]
+            extra = dict(num_layers_total=32, layer_offset=32 - n)
+        else:
+            ref = oracle.METHODS[name](layers[:n], **okw)
+            extra = {}
+        got = fn([(to_dev(k), to_dev(v)) for k, v in layers[:n]],
+                 **{k: v for k, v in kw.items() if k not in ("num_layers_total", "layer_offset")},
+                 **extra)
+        torch.cuda.synchronize()
+        for li, ((ko, vo), (rk, rv, _)) in enumerate(zip(got, ref)):
+            assert ko.shape[2] == rk.shape[2], (name, n, li)
+            assert np.array_equal(to_np(ko), rk) and np.array_equal(to_np(vo), rv), (name, n, li)

@@ -183,3 +183,37 @@ def test_register_heap_matches_serial_heap_select(model):
     model.model_regheap_check.restype = ctypes.c_int
     model.model_regheap_check.argtypes = [ctypes.c_uint64, ctypes.c_int]
     assert model.model_regheap_check(12345, 6000) == 0
+
+
+def test_tiny_chain_lane_model_matches_libstdcxx(model):
+    """wave_tiny_chain (csrc/kvc.hip: the chain's levels on segments of <= 64 positions from
+    registers -- ballots, mbcnt ranks, forward-permute rank tables, backward-permute swaps) as a
+    lane-by-lane model (select_model.cpp tiny_level) gives libstdc++'s first-k set: heavy ties,
+    sort and nth_element, the k boundaries, small rows that enter the tiny levels at once, and the
+    McIlroy adversary (depth-limit fallback from inside the tiny levels)."""
+    model.model_set_tiny.argtypes = [ctypes.c_int]
+    model.model_set_tiny(1)
+    try:
+        rng = np.random.default_rng(11)
+        for trial in range(3000):
+            n = int(rng.integers(4, 70)) if trial % 3 else int(rng.integers(70, 5000))
+            keys = rng.integers(0, int(rng.choice([1, 2, 3, 5, 9, 80, 1 << 16])), n).astype(np.uint32)
+            for k in {1, 2, n // 2, n - 2, n - 1, int(rng.integers(1, n))}:
+                if not 0 < k < n:
+                    continue
+                for topk in (0, 1):
+                    if topk and k * 64 <= n:
+                        continue  # partial_sort: the heap path, no chain
+                    got, _ = run_model(model, keys, k, topk)
+                    np.testing.assert_array_equal(got, ref_set(keys, k, topk),
+                                                  err_msg=f"n={n} k={k} topk={topk}")
+        adv = np.empty(64, dtype=np.int64)
+        for n in (20, 40, 64):
+            for mode in (0, 1):
+                for k in (1, n // 2, n - 1):
+                    oracle.lib().orc_antiqsort(n, mode, k, adv.ctypes.data)
+                    keys = adv[:n].astype(np.uint32)
+                    got, _ = run_model(model, keys, k, mode)
+                    np.testing.assert_array_equal(got, ref_set(keys, k, mode))
+    finally:
+        model.model_set_tiny(0)

@@ -20,6 +20,9 @@
 #   h2olong    rocprofv3 kernel stats of the long h2o_attention call
 #              (tools/h2o_long_profile.py)                                        -> h2oprof/
 #   heap       tools/heap_probe (register heap select vs std::partial_sort)      -> heap_probe.jsonl
+#   gatherprobe  tools/row_gather_probe (160-B row gathers, load shapes) timed, then FETCH_SIZE
+#              and the TCC read-request counters per shape (one rocprofv3 pass each)
+#                                                                                -> gprobe/
 # Every GPU step runs under its own time limit and the first failure ends the call.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"
@@ -125,6 +128,23 @@ for step in "$@"; do
     heap)
       timeout -k 10 120 tools/heap_probe > "$O/heap_probe.jsonl" 2>&1 || { cat "$O/heap_probe.jsonl"; exit 1; }
       cat "$O/heap_probe.jsonl" ;;
+    gatherprobe)
+      G="$O/gprobe"; mkdir -p "$G"
+      timeout -k 10 120 tools/row_gather_probe > "$G/times.json" 2> "$G/times.err" || { cat "$G/times.err"; exit 1; }
+      cat "$G/times.json"
+      ( cd /tmp && export TMPDIR=/tmp && timeout -k 10 60 rocprofv3 -L > "$G/counters.txt" 2>&1 ) || true
+      grep -o -E "TCC_EA0_RDREQ[A-Z0-9_]*|TCC_REQ|TCC_READ|TCC_MISS|TCC_HIT" "$G/counters.txt" | sort -u > "$G/tcc_names.txt" || true
+      cat "$G/tcc_names.txt"
+      passes="FETCH_SIZE"
+      grep -qx TCC_EA0_RDREQ "$G/tcc_names.txt" && grep -qx TCC_EA0_RDREQ_32B "$G/tcc_names.txt" && passes="$passes TCC_EA0_RDREQ_sum,TCC_EA0_RDREQ_32B_sum"
+      grep -qx TCC_MISS "$G/tcc_names.txt" && grep -qx TCC_HIT "$G/tcc_names.txt" && passes="$passes TCC_HIT_sum,TCC_MISS_sum"
+      grep -qx TCC_EA0_RDREQ_64B "$G/tcc_names.txt" && grep -qx TCC_EA0_RDREQ_128B "$G/tcc_names.txt" && passes="$passes TCC_EA0_RDREQ_64B_sum,TCC_EA0_RDREQ_128B_sum"
+      for ps in $passes; do
+        ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 60 rocprofv3 --pmc ${ps//,/ } --output-format csv \
+            -d "$G/pmc_${ps%%,*}" -o run -- "$R/tools/row_gather_probe" 2 > "$G/pmc_${ps%%,*}.log" 2>&1 ) \
+            || { tail "$G/pmc_${ps%%,*}.log"; exit 1; }
+      done
+      python3 tools/pmc_bykernel.py "$G" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

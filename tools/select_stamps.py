@@ -16,7 +16,7 @@ from kvcompress import _native as N  # noqa: E402
 
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(0)
-L, H, D = 32, 32, 128
+L, H, D = int(os.environ.get("SEL_L", "32")), 32, 128  # SEL_L=4: the 8-way split (128 rows)
 S = int(os.environ.get("SEL_S", "16384"))
 k = int(os.environ.get("SEL_K", "512"))
 ALGO = int(os.environ.get("SEL_ALGO", "0"))      # 1: topk (introselect)
@@ -41,7 +41,7 @@ p = N.Params(dtype=DT[1], batch=1, heads=H, head_dim=D, order=ORDER, algo=ALGO,
 rc, info = N.plan(p, table)
 assert rc == 0
 ws = torch.zeros(int(info.workspace_bytes), dtype=torch.uint8, device=dev)
-res = {"wave_seg": "compile-time kWaveSeg", "S": S, "k": k, "algo": ALGO, "order": ORDER,
+res = {"wave_seg": "compile-time kWaveSeg", "layers": L, "S": S, "k": k, "algo": ALGO, "order": ORDER,
        "score_mode": SCORE}
 for rep in range(3):
     rc = N.launch(p, table, ws.data_ptr(), int(info.workspace_bytes),
