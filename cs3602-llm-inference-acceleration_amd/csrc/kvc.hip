@@ -84,11 +84,6 @@ constexpr bool kSgNtl = KVC_SG_NTL;
 #define KVC_TINY_CHAIN 1
 #endif
 constexpr bool kTinyChain = KVC_TINY_CHAIN;
-// partition_level loads s_m with g_{m+1} (single-window levels); 0: after the swaps
-#ifndef KVC_EARLY_CUT
-#define KVC_EARLY_CUT 1
-#endif
-constexpr bool kEarlyCut = KVC_EARLY_CUT;
 struct LayerChunk {
   kvc_layer_t l[kArgLayers];
 };
@@ -1135,6 +1130,16 @@ __device__ int heap_candidates(const K* key, int middle, int len, uint16_t* cand
 // masked and the median slot ch carries klo's flags (kge / kle): the owner wave moves the
 // median physically only after this pass.
 enum { P2_FULL = 0, P2_LEFT = 1, P2_RIGHT = 2 };
+// P2's running rank bases: scalar popcounts (s_bcnt1 + s_add on the CU's one scalar unit, then a
+// v_mov into mbcnt's base operand), or with KVC_P2_VBASE the VALU (two v_bcnt per row, the base
+// a VGPR mbcnt reads directly)
+#ifndef KVC_P2_VBASE
+#define KVC_P2_VBASE 0
+#endif
+__device__ __forceinline__ int p2_count(uint64_t m) {
+  if constexpr (KVC_P2_VBASE) return vpopc(m);
+  else return __popcll(m);
+}
 template <typename KeyT, int JM, bool FAST, int MODE = P2_FULL>
 __device__ __forceinline__ void p2_window0(const KeyT* key, uint16_t* spos, uint16_t* gpos,
                                            int lane, int pos0, int wbeg, int J, int hi,
@@ -1176,12 +1181,12 @@ __device__ __forceinline__ void p2_window0(const KeyT* key, uint16_t* spos, uint
         const uint64_t bg = __builtin_amdgcn_ballot_w64(ge);
         const int a1 = vreg(min(mbcnt(bg, rge1), cap1));
         gpos[ge ? a1 : lane - 64] = (uint16_t)pj;
-        rge1 += __popcll(bg);
+        rge1 += p2_count(bg);
       } else if constexpr (MODE == P2_RIGHT) {
         const uint64_t bl = __builtin_amdgcn_ballot_w64(le);
         const int sr = vreg(min(t1 - 1 - mbcnt(bl, rle), cap1));  // s rank of an le position
         spos[le ? sr : lane - 64] = (uint16_t)pj;
-        rle += __popcll(bl);
+        rle += p2_count(bl);
         if (ff == kBig) {
           const uint64_t bg = __builtin_amdgcn_ballot_w64(ge);
           if (bg) ff = pj - lane + (int)__builtin_ctzll(bg);
@@ -1194,8 +1199,8 @@ __device__ __forceinline__ void p2_window0(const KeyT* key, uint16_t* spos, uint
         gpos[ge ? min(a1, cap1) : lane - 64] = (uint16_t)pj;
         // g_t < s_t  <=>  A + Lin < tot_le  <=>  a1 < sr: swapped (a prefix t <= m of the g's)
         nsw += __popcll(bg & __builtin_amdgcn_ballot_w64(a1 < sr));
-        rge1 += __popcll(bg);
-        rle += __popcll(bl);
+        rge1 += p2_count(bg);
+        rle += p2_count(bl);
       }
     });
   });
@@ -1441,9 +1446,6 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
   }
   // g_{m+1}, the first unswapped ge position (none when every ge position is swapped)
   int gnext = msw >= tot_ge ? kBig : msw < cap ? uni((int)gpos[msw + 1]) : kBig;
-  // s_m of a single-window level (msw <= cap: P4 never rewrites the tables), loaded beside
-  // g_{m+1} instead of after the swaps' barrier
-  const int s_m = kEarlyCut && msw > 0 && msw <= cap ? uni((int)spos[msw]) : kBig;
   KVC_TICK(t2);
   // ---- m >= cap (rare): the level's flags, from the keys before any swap (the median slot is
   // physical now), kept in registers for the later windows' scatters (the swapped pairs are
@@ -1575,7 +1577,6 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
     }
   }
 #endif
-  if (kEarlyCut && msw <= cap) return min(gnext, s_m);
   return min(gnext, msw > 0 ? uni((int)spos[msw - wb]) : kBig);
 }
 

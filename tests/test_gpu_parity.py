@@ -532,3 +532,39 @@ def test_few_rows_split_copy_matches_oracle(name, kw, dt):
         for li, ((ko, vo), (rk, rv, _)) in enumerate(zip(got, ref)):
             assert ko.shape[2] == rk.shape[2], (name, n, li)
             assert np.array_equal(to_np(ko), rk) and np.array_equal(to_np(vo), rv), (name, n, li)
+
+
+def _neg16(nrm):
+    """-x of non-negative 16-bit norms in storage representation (bf16 bits / float16)."""
+    return nrm ^ np.uint16(0x8000) if nrm.dtype == np.uint16 else -nrm
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_abi_tiny_segments_and_adversaries(dtype, mode):
+    """The chain's last levels on segments of <= 64 positions run from registers
+    (wave_tiny_chain): whole rows of 5..200 positions (tie-heavy and McIlroy-adversary keys, so
+    the introsort / introselect depth limit falls inside those levels and the serial heap
+    fallback takes over from the registers), 16-bit keys, sort and topk (ascending: the
+    oracle's topk of the negated norms), against the oracle."""
+    def ref_of(nrm, k):
+        if mode == 0:
+            return np.sort(oracle.argsort_prefix(nrm, k), axis=-1)
+        return np.sort(oracle.topk_indices(_neg16(nrm), k), axis=-1)
+    for n in (5, 17, 33, 64, 65, 100, 200):
+        K = prng.gen_keys(8800 + n, (1, 4, n, 64), dtype, "few")
+        for k in sorted({1, 2, n // 3, n // 2, n - 2, n - 1}):
+            if not 0 < k < n or (mode and k * 64 <= n):
+                continue
+            nrm, idx = _abi_select(K, k, 0, mode)
+            np.testing.assert_array_equal(idx, ref_of(nrm, k), err_msg=f"few n={n} k={k}")
+    adv = np.empty(256, dtype=np.int64)
+    for n in (20, 40, 64, 100, 200):
+        for k in sorted({1, n // 3, n // 2, n - 1}):
+            if mode and k * 64 <= n:
+                continue
+            oracle.lib().orc_antiqsort(n, mode, k, adv.ctypes.data)
+            K = np.zeros((1, 1, n, 64), dtype=np.float32)
+            K[0, 0, :, 0] = (adv[:n] + 1).astype(np.float32)  # exact in bf16 / fp16 (<= 256)
+            nrm, idx = _abi_select(prng.to_dtype(K, dtype), k, 0, mode)
+            np.testing.assert_array_equal(idx, ref_of(nrm, k), err_msg=f"adversary n={n} k={k}")

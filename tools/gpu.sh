@@ -20,6 +20,8 @@
 #   h2olong    rocprofv3 kernel stats of the long h2o_attention call
 #              (tools/h2o_long_profile.py)                                        -> h2oprof/
 #   heap       tools/heap_probe (register heap select vs std::partial_sort)      -> heap_probe.jsonl
+#   sq:LIB     SQ issue / wait counters of the headline SELECT_GATHER kernel with library LIB
+#              (kvcompress/_lib/LIB.so; two rocprofv3 --pmc passes of 8 SQ counters) -> sq_LIB.json
 #   gatherprobe  tools/row_gather_probe (160-B row gathers, load shapes) timed, then FETCH_SIZE
 #              and the TCC read-request counters per shape (one rocprofv3 pass each)
 #                                                                                -> gprobe/
@@ -145,6 +147,18 @@ for step in "$@"; do
             || { tail "$G/pmc_${ps%%,*}.log"; exit 1; }
       done
       python3 tools/pmc_bykernel.py "$G" ;;
+    sq:*)
+      lib="${step#sq:}"
+      for set in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS" \
+                 "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES"; do
+        tag="sq_${lib}_${set%% *}"
+        ( cd /tmp && export TMPDIR=/tmp && KVC_LIB="$LIBDIR/$lib.so" timeout -s KILL 120 rocprofv3 --pmc $set \
+            --kernel-include-regex "select_gather" --output-format csv -d "$O/$tag" -o run \
+            -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$O/$tag.log" 2>&1 ) \
+            || { tail "$O/$tag.log"; exit 1; }
+      done
+      python3 tools/pmc_summary.py "$O/sq_${lib}_SQ_WAVE_CYCLES" "$O/sq_${lib}_SQ_LDS_BANK_CONFLICT" > "$O/sq_$lib.json" \
+          && cat "$O/sq_$lib.json" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
