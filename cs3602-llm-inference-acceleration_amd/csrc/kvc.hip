@@ -52,7 +52,10 @@ constexpr long kBigBudget = 81408;    // 2 x (this + scalars) <= 160 KiB
 constexpr int kZoneMax = 16384;        // longest zone whose selection runs from LDS
 constexpr int kZoneMaxGlobal = 65536;  // longest zone of the u16-position global variant
 constexpr int kZoneMaxLong = 1 << 24;   // longest zone at all (u32 positions; global scratch)
-constexpr int kWaveSeg = 256;  // segments this short are finished by one wave (64 / 128 / 512 / 1024 measured slower)
+#ifndef KVC_WAVE_SEG
+#define KVC_WAVE_SEG 256
+#endif
+constexpr int kWaveSeg = KVC_WAVE_SEG;  // segments this short are finished by one wave (64 / 128 / 512 / 1024 measured slower)
 // the same for 512-thread rows (128 / 512 / 1 024 measured the same or slower at S = 4 096 and
 // 8 192: profiles/r03_g_small_wave_threshold_ab.jsonl)
 constexpr int kWaveSegSmall = 256;
