@@ -1,0 +1,114 @@
+"""evaluate_with_attention_compression / compare_h2o_methods (reference:
+kvcompress/evaluate_attention.py) on a small random-weight GPT-NeoX.
+
+CPU: the harness runs end to end with the numpy oracle standing in for the manager and the
+compress call (test infrastructure), real attention weights reach the manager although the model
+is configured for sdpa, and the model's attention implementation is restored afterwards.
+GPU: the engine's manager + h2o_attention_compress against the oracle's -- identical caches at
+every step, so the PPL and accuracy match exactly (PPL delta 0), in fp32 / bf16 / fp16."""
+import numpy as np
+import pytest
+import torch
+
+from gpu_util import to_dev, to_np
+from oracle import h2o_oracle as HO
+from test_ppl_parity import TEXT, ToyTokenizer, toy_model
+
+KW = dict(start_size=4, heavy_hitter_size=16, recent_size=40)
+THREADS = 8  # reduction order of both managers' sums
+
+
+class OracleManager:
+    """The oracle's H2OManager behind the reference manager's interface (torch in, numpy
+    state)."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+        self.updates = 0
+        self.reset()
+
+    def reset(self):
+        self.m = HO.H2OManager(threads=THREADS, **self.kw)
+
+    def update_attention_scores(self, attentions, skip_layers=()):
+        if attentions is not None and len(attentions):
+            self.updates += 1
+        self.m.update_attention_scores(
+            None if attentions is None else [None if a is None else to_np(a)
+                                             for a in attentions], skip_layers)
+
+
+def oracle_compress(kv_list, attention_scores=None, h2o_manager=None, **kw):
+    dev = kv_list[0][0].device
+    atts = None if attention_scores is None else [None if a is None else to_np(a)
+                                                  for a in attention_scores]
+    if h2o_manager is not None and atts is not None:
+        h2o_manager.m.update_attention_scores(atts, kw.get("skip_layers", ()))
+    out = HO.h2o_attention_compress([(to_np(k), to_np(v)) for k, v in kv_list], None,
+                                    h2o_manager.m if h2o_manager is not None else None, **kw)
+    return [(k, v) if kind == "same" else (to_dev(ko, dev), to_dev(vo, dev))
+            for (k, v), (ko, vo, kind) in zip(kv_list, out)]
+
+
+def _run_oracle(model, tok, max_tokens, monkeypatch, **kw):
+    from kvcompress import evaluate_attention as EA
+    monkeypatch.setattr(EA, "h2o_attention_compress", oracle_compress)
+    mgr = OracleManager(**kw)
+    r = EA.evaluate_with_attention_compression(model, tok, TEXT, h2o_manager=mgr,
+                                               max_tokens=max_tokens, skip_layers=[0],
+                                               show_progress=False, **kw)
+    monkeypatch.undo()
+    return r, mgr
+
+
+def test_harness_runs_with_oracle_on_cpu(monkeypatch):
+    model = toy_model(torch.float32, "cpu", layers=2)
+    assert model.config._attn_implementation == "sdpa"
+    tok = ToyTokenizer(512)
+    r, mgr = _run_oracle(model, tok, 120, monkeypatch, **KW)
+    assert model.config._attn_implementation == "sdpa"  # restored
+    assert mgr.updates == 119  # every step's attention weights reached the manager
+    assert r["num_tokens"] == 119
+    assert r["final_cache_size"] == sum(KW.values())
+    assert np.isfinite(r["perplexity"]) and 0.0 <= r["accuracy"] <= 1.0
+    assert set(r) == {"perplexity", "accuracy", "num_tokens", "final_cache_size", "ttft",
+                      "tpot", "throughput", "total_time"}
+
+
+def test_short_text_returns_reference_empty_result():
+    from kvcompress.evaluate_attention import evaluate_with_attention_compression
+    model = toy_model(torch.float32, "cpu", layers=1)
+    r = evaluate_with_attention_compression(model, ToyTokenizer(512), "a",
+                                            h2o_manager=OracleManager(**KW), show_progress=False)
+    assert r["perplexity"] == float("inf") and r["num_tokens"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+def test_ppl_delta_zero_engine_vs_oracle(dtype, monkeypatch):
+    from kvcompress.evaluate_attention import evaluate_with_attention_compression
+    from kvcompress.methods.h2o_attention import create_h2o_manager_from_model
+    from kvcompress import _engine
+    model = toy_model(dtype, "cuda:0")
+    tok = ToyTokenizer(512)
+    mgr = create_h2o_manager_from_model(model, **KW)
+    mgr.reduction_threads = THREADS
+    a = evaluate_with_attention_compression(model, tok, TEXT, h2o_manager=mgr, max_tokens=300,
+                                            skip_layers=[0], show_progress=False, **KW)
+    b, _ = _run_oracle(model, tok, 300, monkeypatch, **KW)
+    assert a["final_cache_size"] == b["final_cache_size"] == sum(KW.values())
+    assert a["perplexity"] == b["perplexity"], (a["perplexity"], b["perplexity"])
+    assert a["accuracy"] == b["accuracy"]
+    assert _engine.device_status(0) == 0
+
+
+@pytest.mark.gpu
+def test_compare_h2o_methods_runs_on_engine():
+    from kvcompress.evaluate_attention import compare_h2o_methods
+    model = toy_model(torch.bfloat16, "cuda:0", layers=3)
+    res = compare_h2o_methods(model, ToyTokenizer(512), TEXT * 2, max_tokens=560,
+                              heavy_hitter_sizes=[32], skip_layers=[0])
+    assert [r["method"] for r in res] == ["baseline", "h2o_l2_hh32", "h2o_attention_hh32"]
+    assert res[0]["final_cache_size"] == 559
+    assert res[1]["final_cache_size"] == res[2]["final_cache_size"] == 512
+    assert all(np.isfinite(r["perplexity"]) for r in res)
