@@ -349,9 +349,15 @@ def status_word(device):
     Read it with device_status()."""
     w = _status_words.get(device)
     if w is None:
-        w = torch.zeros(1, dtype=torch.int32, device=torch.device("cuda", device))
-        _status_words[device] = w
+        w = _status_words[device] = _new_status_word(device)
     return w
+
+
+def _new_status_word(device):
+    # a normal tensor even when the first call comes inside torch.inference_mode() (the
+    # evaluation loops): device_status(clear=True) zeroes it in place from any mode
+    with torch.inference_mode(False):
+        return torch.zeros(1, dtype=torch.int32, device=torch.device("cuda", device))
 
 
 def device_status(device=None, clear=False):

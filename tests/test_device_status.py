@@ -116,3 +116,15 @@ def test_opt_in_status_check_raises_naming_the_bit():
         fix_size_l2_compress(layers, fix_kv_size=512, skip_layers=[])
     finally:
         E.set_status_check(prev)
+
+
+def test_status_word_first_made_inside_inference_mode_stays_clearable():
+    """The evaluation loops run under torch.inference_mode(); a status word first created there
+    must still be a normal tensor, which device_status(clear=True) zeroes in place afterwards."""
+    from kvcompress import _engine as E
+    with torch.inference_mode():
+        w = E._new_status_word(0)
+    assert not w.is_inference()
+    w.zero_()
+    torch.cuda.synchronize()
+    assert int(w.item()) == 0
