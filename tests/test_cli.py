@@ -61,3 +61,31 @@ def test_cli_end_to_end_on_gpu(capsys):
         assert np.isfinite(r["perplexity"])
     assert res[1]["final_cache_size"] == 32 and res[2]["final_cache_size"] == 32
     assert "Benchmark completed!" in capsys.readouterr().out
+
+
+H2O_CLI = os.path.join(ROOT, "cs3602-llm-inference-acceleration_amd", "scripts",
+                       "test_h2o_attention.py")
+
+
+def _h2o_cli():
+    spec = importlib.util.spec_from_file_location("kvc_h2o_cli", H2O_CLI)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_h2o_cli_defaults_match_reference():
+    """scripts/test_h2o_attention.py:95-107 of the reference: argument names and defaults."""
+    a = _h2o_cli().build_parser().parse_args([])
+    assert (a.model_id, a.max_tokens, a.heavy_hitter_sizes, a.compare, a.skip_layers) == \
+        ("EleutherAI/pythia-2.8b", 1500, "32,64,128", False, "0,1")
+
+
+@pytest.mark.gpu
+def test_h2o_cli_compare_on_gpu(capsys):
+    mod = _h2o_cli()
+    mod.main(["--random_model", "pythia-tiny", "--synthetic_text", "--compare", "--max_tokens",
+              "560", "--heavy_hitter_sizes", "32", "--skip_layers", "0"])
+    out = capsys.readouterr().out
+    assert "h2o_attention_hh32" in out and "H2O-Attention:" in out
+    assert "Test completed!" in out
