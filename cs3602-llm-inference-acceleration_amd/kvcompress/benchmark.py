@@ -6,7 +6,7 @@ from typing import Callable, Dict, List, Optional
 import torch
 
 from .evaluate import evaluate_with_compression
-from .utils import normalize_kv_cache, to_dynamic_cache
+from .utils import key_length_attention, normalize_kv_cache, to_dynamic_cache
 
 
 def measure_generation_metrics(model, tokenizer, text: str, compress_fn: Optional[Callable] = None,
@@ -30,7 +30,7 @@ def measure_generation_metrics(model, tokenizer, text: str, compress_fn: Optiona
                                             skip_layers=skip_layers, **compress_kwargs))
 
     t_start = time.perf_counter()
-    with torch.inference_mode():
+    with torch.inference_mode(), key_length_attention(model):
         t0 = time.perf_counter()
         out = model(ids, use_cache=True, return_dict=True)
         tok = torch.argmax(out.logits[:, -1, :], dim=-1, keepdim=True)

@@ -4,7 +4,9 @@ Same functions, arguments and result keys as the reference's kvcompress/evaluate
 works with transformers >= 5 caches (the reference's loop cannot unpack them).
 One token per forward; after every forward the cache is normalised to a (K, V) list, compressed
 by `compress_fn(kv_list, skip_layers=..., **compress_kwargs)` (the MI355X engine when it is one of
-this package's methods) and rebuilt as a DynamicCache.
+this package's methods) and rebuilt as a DynamicCache.  A model configured for eager attention
+runs utils.key_length_attention's kvc_eager meanwhile (transformers 5's eager kernel cannot take
+layers of different lengths).
 """
 import time
 from typing import Callable, Dict, List, Optional
@@ -12,7 +14,7 @@ from typing import Callable, Dict, List, Optional
 import torch
 from torch.nn import CrossEntropyLoss
 
-from .utils import normalize_kv_cache, to_dynamic_cache
+from .utils import key_length_attention, normalize_kv_cache, to_dynamic_cache
 
 
 def _progress(it, show):
@@ -44,7 +46,7 @@ def evaluate_with_compression(model, tokenizer, text: str, compress_fn: Optional
     model.eval()
     steps = _progress(range(n - 1), show_progress)
     t_start = time.perf_counter()
-    with torch.inference_mode():
+    with torch.inference_mode(), key_length_attention(model):
         for i in steps:
             t0 = time.perf_counter()
             out = model(ids[:, i:i + 1], past_key_values=cache, use_cache=True)

@@ -12,12 +12,10 @@ transformers >= 5 returns no attention weights from the sdpa / flash kernels (th
 the reference ran on fell back to eager attention by themselves), and its eager attention adds the
 causal mask without cutting it to the layer's key length -- a mask built for the uncompressed
 skip layers no longer fits the compressed ones.  For the duration of the call the model runs
-"kvc_eager": the model's own eager attention with the mask cut to the keys, as the 4.x eager
-kernels did (attention_mask[:, :, :, :key_len]); the previous implementation is restored after.
+"kvc_eager" (utils.key_length_attention): the model's own eager attention with the mask cut to
+the keys, as the 4.x eager kernels did; the previous implementation is restored after.
 """
-import sys
 import time
-from contextlib import contextmanager
 from typing import Dict, List, Optional
 
 import torch
@@ -25,48 +23,10 @@ from torch.nn import CrossEntropyLoss
 
 from .evaluate import _progress
 from .methods.h2o_attention import H2OAttentionManager, h2o_attention_compress
-from .utils import normalize_kv_cache, to_dynamic_cache
+from .utils import key_length_attention, normalize_kv_cache, to_dynamic_cache
 
 _EMPTY = {"perplexity": float("inf"), "accuracy": 0.0, "num_tokens": 0, "final_cache_size": 0,
           "ttft": 0.0, "tpot": 0.0, "throughput": 0.0, "total_time": 0.0}
-
-
-EAGER = "kvc_eager"
-
-
-def _eager_forward(module, query, key, value, attention_mask, **kwargs):
-    """The attention module's own eager_attention_forward (llama's for a model file without
-    one), the mask cut to this layer's key length."""
-    fn = getattr(sys.modules.get(type(module).__module__), "eager_attention_forward", None)
-    if fn is None:
-        from transformers.models.llama.modeling_llama import eager_attention_forward as fn
-    if attention_mask is not None and attention_mask.shape[-1] != key.shape[-2]:
-        attention_mask = attention_mask[..., :key.shape[-2]]
-    return fn(module, query, key, value, attention_mask, **kwargs)
-
-
-def _register_eager():
-    from transformers import AttentionInterface
-    from transformers.masking_utils import ALL_MASK_ATTENTION_FUNCTIONS, AttentionMaskInterface
-    if EAGER not in ALL_MASK_ATTENTION_FUNCTIONS:
-        AttentionInterface.register(EAGER, _eager_forward)
-        AttentionMaskInterface.register(EAGER, ALL_MASK_ATTENTION_FUNCTIONS["eager"])
-
-
-@contextmanager
-def _eager_attention(model):
-    """The model with attention weights available (kvc_eager) inside the block."""
-    cfg = getattr(model, "config", None)
-    impl = getattr(cfg, "_attn_implementation", None)
-    switch = impl not in (None, EAGER) and hasattr(model, "set_attn_implementation")
-    if switch:
-        _register_eager()
-        model.set_attn_implementation(EAGER)
-    try:
-        yield
-    finally:
-        if switch:
-            model.set_attn_implementation(impl)
 
 
 def evaluate_with_attention_compression(model, tokenizer, text: str,
@@ -95,7 +55,7 @@ def evaluate_with_attention_compression(model, tokenizer, text: str,
     model.eval()
     steps = _progress(range(n - 1), show_progress)
     t_start = time.perf_counter()
-    with torch.inference_mode(), _eager_attention(model):
+    with torch.inference_mode(), key_length_attention(model, need_weights=True):
         for i in steps:
             t0 = time.perf_counter()
             out = model(ids[:, i:i + 1], past_key_values=cache, use_cache=True,

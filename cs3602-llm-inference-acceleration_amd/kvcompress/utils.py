@@ -4,6 +4,8 @@
 reference cannot unpack; for tuple lists and legacy caches it returns what
 the reference returns.
 """
+import sys
+from contextlib import contextmanager
 from typing import List, Tuple
 
 import torch
@@ -69,6 +71,55 @@ def get_seq_len(past_key_values, layer_idx: int = 0) -> int:
         return 0
     return layers[layer_idx][0].size(2)  # negative indices count from the end, as there
 
+
+
+# ---------------------------------------------------------------------------------------------
+# Attention with per-layer key lengths under transformers >= 5.  Compressed caches give layers
+# different lengths (skip_layers keep everything).  transformers 4.x -- which the reference ran
+# on -- cut the causal mask to each layer's keys in its eager kernels
+# (attention_mask[:, :, :, :key_len]); 5.x eager adds the mask built for the longest layer as is
+# and raises, and 5.x sdpa / flash return no attention weights.  "kvc_eager" is the model's own
+# eager attention with the 4.x cut.
+# ---------------------------------------------------------------------------------------------
+KEY_LENGTH_EAGER = "kvc_eager"
+
+
+def _eager_forward(module, query, key, value, attention_mask, **kwargs):
+    """The attention module's own eager_attention_forward (llama's for a model file without
+    one), the mask cut to this layer's key length."""
+    fn = getattr(sys.modules.get(type(module).__module__), "eager_attention_forward", None)
+    if fn is None:
+        from transformers.models.llama.modeling_llama import eager_attention_forward as fn
+    if attention_mask is not None and attention_mask.shape[-1] != key.shape[-2]:
+        attention_mask = attention_mask[..., :key.shape[-2]]
+    return fn(module, query, key, value, attention_mask, **kwargs)
+
+
+def _register_eager():
+    from transformers import AttentionInterface
+    from transformers.masking_utils import ALL_MASK_ATTENTION_FUNCTIONS, AttentionMaskInterface
+    if KEY_LENGTH_EAGER not in ALL_MASK_ATTENTION_FUNCTIONS:
+        AttentionInterface.register(KEY_LENGTH_EAGER, _eager_forward)
+        AttentionMaskInterface.register(KEY_LENGTH_EAGER, ALL_MASK_ATTENTION_FUNCTIONS["eager"])
+
+
+@contextmanager
+def key_length_attention(model, need_weights: bool = False):
+    """Inside the block the model runs kvc_eager when it is configured for eager attention, or
+    for any implementation when `need_weights` (output_attentions); its previous implementation
+    is restored on exit.  Models without set_attn_implementation (transformers 4.x) are left
+    alone: their eager kernels already cut the mask."""
+    impl = getattr(getattr(model, "config", None), "_attn_implementation", None)
+    switch = (hasattr(model, "set_attn_implementation") and impl is not None and
+              impl != KEY_LENGTH_EAGER and (need_weights or impl == "eager"))
+    if switch:
+        _register_eager()
+        model.set_attn_implementation(KEY_LENGTH_EAGER)
+    try:
+        yield
+    finally:
+        if switch:
+            model.set_attn_implementation(impl)
 
 __all__ = ["to_dynamic_cache", "normalize_kv_cache", "get_cache_size_mb", "get_cache_info",
            "get_seq_len"]

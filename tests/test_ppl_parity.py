@@ -85,3 +85,26 @@ def test_ppl_delta_zero_engine_vs_oracle(dtype, name, kw):
     assert a["final_cache_size"] == b["final_cache_size"]
     assert a["perplexity"] == b["perplexity"], (a["perplexity"], b["perplexity"])
     assert a["accuracy"] == b["accuracy"]
+
+
+def test_eager_model_with_compressed_layers_runs_on_cpu():
+    """transformers 5's eager attention adds a mask sized for the longest layer; the harness
+    runs such a model through utils.key_length_attention (the 4.x mask cut) and restores its
+    implementation.  Its PPL agrees with the sdpa run of the same model (fp32, 1e-4)."""
+    from kvcompress.benchmark import measure_generation_metrics
+    from kvcompress.evaluate import evaluate_with_compression
+    model = toy_model(torch.float32, "cpu", layers=2)
+    tok = ToyTokenizer(512)
+    kw = dict(compress_fn=oracle_compress("fix_size_l2"), compress_kwargs=dict(fix_kv_size=32),
+              skip_layers=[0])
+    sdpa = evaluate_with_compression(model, tok, TEXT[:200], max_tokens=120, show_progress=False,
+                                     **kw)
+    model.set_attn_implementation("eager")
+    eager = evaluate_with_compression(model, tok, TEXT[:200], max_tokens=120, show_progress=False,
+                                      **kw)
+    assert model.config._attn_implementation == "eager"
+    assert eager["final_cache_size"] == sdpa["final_cache_size"] == 32
+    assert abs(eager["perplexity"] / sdpa["perplexity"] - 1) < 1e-4
+    g = measure_generation_metrics(model, tok, TEXT[:200], max_new_tokens=40, max_input_tokens=60,
+                                   **kw)
+    assert g["num_tokens"] == 40 and model.config._attn_implementation == "eager"
