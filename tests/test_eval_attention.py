@@ -5,14 +5,14 @@ CPU: the harness runs end to end with the numpy oracle standing in for the manag
 compress call (test infrastructure), real attention weights reach the manager although the model
 is configured for sdpa, and the model's attention implementation is restored afterwards.
 GPU: the engine's manager + h2o_attention_compress against the oracle's -- identical caches at
-every step, so the PPL and accuracy match exactly (PPL delta 0), in fp32 / bf16 / fp16."""
+every step, so the PPL and accuracy match exactly (PPL delta 0), in fp32 / bf16 / fp16, and for a grouped-query Llama."""
 import numpy as np
 import pytest
 import torch
 
 from gpu_util import to_dev, to_np
 from oracle import h2o_oracle as HO
-from test_ppl_parity import TEXT, ToyTokenizer, toy_model
+from test_ppl_parity import TEXT, ToyTokenizer, gqa_model, toy_model
 
 KW = dict(start_size=4, heavy_hitter_size=16, recent_size=40)
 THREADS = 8  # reduction order of both managers' sums
@@ -75,6 +75,13 @@ def test_harness_runs_with_oracle_on_cpu(monkeypatch):
                       "tpot", "throughput", "total_time"}
 
 
+def test_gqa_model_runs_with_oracle_on_cpu(monkeypatch):
+    model = gqa_model(torch.float32, "cpu", layers=2)
+    r, mgr = _run_oracle(model, ToyTokenizer(512), 100, monkeypatch, **KW)
+    assert mgr.updates == 99 and r["final_cache_size"] == sum(KW.values())
+    assert np.isfinite(r["perplexity"])
+
+
 def test_short_text_returns_reference_empty_result():
     from kvcompress.evaluate_attention import evaluate_with_attention_compression
     model = toy_model(torch.float32, "cpu", layers=1)
@@ -96,6 +103,27 @@ def test_ppl_delta_zero_engine_vs_oracle(dtype, monkeypatch):
     a = evaluate_with_attention_compression(model, tok, TEXT, h2o_manager=mgr, max_tokens=300,
                                             skip_layers=[0], show_progress=False, **KW)
     b, _ = _run_oracle(model, tok, 300, monkeypatch, **KW)
+    assert a["final_cache_size"] == b["final_cache_size"] == sum(KW.values())
+    assert a["perplexity"] == b["perplexity"], (a["perplexity"], b["perplexity"])
+    assert a["accuracy"] == b["accuracy"]
+    assert _engine.device_status(0) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_gqa_ppl_delta_zero_engine_vs_oracle(dtype, monkeypatch):
+    """Grouped-query attention: heavy hitters from 4-head accumulations select rows of 2-head
+    K / V caches (one index list per layer, shared by the heads)."""
+    from kvcompress.evaluate_attention import evaluate_with_attention_compression
+    from kvcompress.methods.h2o_attention import create_h2o_manager_from_model
+    from kvcompress import _engine
+    model = gqa_model(dtype, "cuda:0")
+    tok = ToyTokenizer(512)
+    mgr = create_h2o_manager_from_model(model, **KW)
+    mgr.reduction_threads = THREADS
+    a = evaluate_with_attention_compression(model, tok, TEXT, h2o_manager=mgr, max_tokens=240,
+                                            skip_layers=[0], show_progress=False, **KW)
+    b, _ = _run_oracle(model, tok, 240, monkeypatch, **KW)
     assert a["final_cache_size"] == b["final_cache_size"] == sum(KW.values())
     assert a["perplexity"] == b["perplexity"], (a["perplexity"], b["perplexity"])
     assert a["accuracy"] == b["accuracy"]

@@ -31,6 +31,17 @@ def toy_model(dtype, device, layers=4, heads=4, head_dim=64, vocab=512):
     return GPTNeoXForCausalLM(cfg).to(dtype).to(device).eval()
 
 
+def gqa_model(dtype, device, layers=3):
+    """A tiny random-weight Llama with grouped-query attention: 4 query heads over 2 K/V heads
+    (head_dim 64), the other cache geometry transformers models hand the methods."""
+    from transformers import LlamaConfig, LlamaForCausalLM
+    torch.manual_seed(0)
+    cfg = LlamaConfig(vocab_size=512, hidden_size=256, intermediate_size=512,
+                      num_hidden_layers=layers, num_attention_heads=4, num_key_value_heads=2,
+                      max_position_embeddings=4096)
+    return LlamaForCausalLM(cfg).to(dtype).to(device).eval()
+
+
 def oracle_compress(name):
     """compress_fn backed by the CPU oracle (test infrastructure)."""
     def fn(kv_list, **kw):
@@ -108,3 +119,19 @@ def test_eager_model_with_compressed_layers_runs_on_cpu():
     g = measure_generation_metrics(model, tok, TEXT[:200], max_new_tokens=40, max_input_tokens=60,
                                    **kw)
     assert g["num_tokens"] == 40 and model.config._attn_implementation == "eager"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,kw", [c for c in CASES if c[0] in
+                                     ("fix_size_l2", "snapkv_lite", "pyramid_kv", "h2o_l2")])
+def test_gqa_ppl_delta_zero_engine_vs_oracle(name, kw):
+    from kvcompress.evaluate import evaluate_with_compression
+    from kvcompress.methods import get_compress_fn
+    model = gqa_model(torch.bfloat16, "cuda:0")
+    tok = ToyTokenizer(512)
+    a, b = (evaluate_with_compression(model, tok, TEXT, compress_fn=fn, compress_kwargs=kw,
+                                      max_tokens=240, skip_layers=[0], show_progress=False)
+            for fn in (get_compress_fn(name), oracle_compress(name)))
+    assert a["final_cache_size"] == b["final_cache_size"]
+    assert a["perplexity"] == b["perplexity"], (a["perplexity"], b["perplexity"])
+    assert a["accuracy"] == b["accuracy"]
