@@ -513,6 +513,9 @@ def main():
         dump_first_layer(args.dump_layer, rank, l0, layers, step())
     if rank == 0:
         res["tokens_evicted_per_sec"] = ev * world * args.steps / elapsed
+        from kvcompress import _engine as _E
+        if _E.tie_policy != "reference":  # KVC_TIE_POLICY=stable: not the reference's tie order
+            res["config"]["tie_policy"] = _E.tie_policy
         if shard:
             res["config"]["as_shard"] = f"rank {shard[0]} of {shard[1]} (layers {l0}-{l1 - 1})"
             res["n_gpus"] = 1

@@ -1870,6 +1870,149 @@ __device__ __forceinline__ bool select_fast_untied(const KeyT* key, int n, int k
   return true;
 }
 
+// KVC_ALGO_STABLE (opt-in, not the reference's tie order): the first k of a STABLE sort of the
+// row's keys -- every key below T, the k-th smallest key, then the first k - #(key < T) keys
+// equal to T in position order.  T by the radix select of select_fast_untied (8-bit digits of
+// key - min from the top, a 256-bin LDS histogram per digit in `hist`, 512 ints) or, for rows
+// whose scratch is shorter, by bisection over the key range; then one counting pass and the
+// ascending emission (output slot of a kept position = #(key < T before it) + min(#(key == T
+// before it), need)).  The keys stay in LDS (read once per pass, nothing held in registers);
+// `sel` must not alias them.
+template <int NT, typename KeyT, bool TO_LDS>
+__device__ __forceinline__ void stable_select(const KeyT* key, int n, int k, SelScalars<KeyT>& sc,
+                                              int32_t* out, uint16_t* sel, int* hist, bool radix) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = (NT == 64) ? 0 : uni(tid >> 6);
+  const int J = (n + NT - 1) / NT;  // positions wid*J*64 + j*64 + lane, j < J, per wave
+  const int wbeg = wid * J * 64;
+  uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+  for (int j = 0; j < J; ++j) {
+    const int pos = wbeg + j * 64 + lane;
+    if (pos < n) {
+      const uint32_t x = (uint32_t)key[pos];
+      mn = min(mn, x);
+      mx = max(mx, x);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+    mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+  }
+  if (lane == 0) {
+    sc.wa[wid] = (int)mn;
+    sc.wb[wid] = (int)mx;
+  }
+  __syncthreads();
+  uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    lo = min(lo, (uint32_t)sc.wa[w]);
+    hi = max(hi, (uint32_t)sc.wb[w]);
+  }
+  lo = (uint32_t)uni((int)lo);
+  hi = (uint32_t)uni((int)hi);
+  __syncthreads();  // sc.wa / sc.wb are reused below
+  int parity = 0;
+  if (radix) {
+    int rem = hi - lo ? 32 - __builtin_clz(hi - lo) : 0;  // offset bits still undecided
+    uint32_t prefix = 0;
+    int below = 0;
+    for (int i = tid; i < 512; i += NT) hist[i] = 0;
+    __syncthreads();
+    while (rem > 0) {
+      const int w = min(8, rem), sh = rem - w;
+      int* h = hist + 256 * parity;
+      for (int j = 0; j < J; ++j) {
+        const int pos = wbeg + j * 64 + lane;
+        if (pos < n) {
+          const uint32_t d = (uint32_t)key[pos] - lo;
+          if ((uint32_t)((uint64_t)d >> rem) == prefix) lds_add1(h + ((d >> sh) & ((1u << w) - 1u)));
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (int i = tid; i < 256; i += NT) hist[256 * (parity ^ 1) + i] = 0;
+      __syncthreads();
+      if (wid == 0) {
+        const int c0 = h[4 * lane], c1 = h[4 * lane + 1], c2 = h[4 * lane + 2],
+                  c3 = h[4 * lane + 3];
+        const int s4 = c0 + c1 + c2 + c3;
+        const int ex = block_exclusive_scan<64>(s4, nullptr, lane, 0);
+        const int need = k - below;  // >= 1: the k-th key lies in this bucket
+        const uint64_t b = __builtin_amdgcn_ballot_w64(ex + s4 >= need);
+        if (lane == (b ? __builtin_ctzll(b) : 63)) {
+          int c = ex, bin = 4 * lane;
+          if (c + c0 < need) {
+            c += c0; ++bin;
+            if (c + c1 < need) {
+              c += c1; ++bin;
+              if (c + c2 < need) { c += c2; ++bin; }
+            }
+          }
+          sc.wa[0] = bin;
+          sc.wb[0] = below + c;
+        }
+      }
+      __syncthreads();
+      prefix = (prefix << w) | (uint32_t)sc.wa[0];
+      below = sc.wb[0];
+      rem = sh;
+      parity ^= 1;
+      __syncthreads();  // sc.wa[0] / sc.wb[0] are rewritten by the next pass
+    }
+    lo = lo + prefix;
+  }
+  // smallest v with #(key <= v) >= k (bisection; the radix select leaves lo == hi's answer)
+  while (!radix && lo < hi) {
+    const uint32_t mid = lo + ((hi - lo) >> 1);
+    int cl = 0;
+    for (int j = 0; j < J; ++j) {
+      const int pos = wbeg + j * 64 + lane;
+      cl += (pos < n && (uint32_t)key[pos] <= mid) ? 1 : 0;
+    }
+    const int rs = row_scan16(cl);
+    const int c = __builtin_amdgcn_readlane(rs, 15) + __builtin_amdgcn_readlane(rs, 31) +
+                  __builtin_amdgcn_readlane(rs, 47) + __builtin_amdgcn_readlane(rs, 63);
+    const int tot = block_sum_waves<NT>(c, parity ? sc.wb : sc.wa, lane, wid);
+    parity ^= 1;
+    if (tot >= k) hi = mid;
+    else lo = mid + 1;
+  }
+  const uint32_t T = lo;
+  int clt = 0, ceq = 0;
+  for (int j = 0; j < J; ++j) {
+    const int pos = wbeg + j * 64 + lane;
+    const uint32_t x = pos < n ? (uint32_t)key[pos] : 0u;
+    clt += __popcll(__builtin_amdgcn_ballot_w64(pos < n && x < T));
+    ceq += __popcll(__builtin_amdgcn_ballot_w64(pos < n && x == T));
+  }
+  if (lane == 0) sc.wm[wid] = clt | (ceq << 16);  // each <= kZoneMax < 2^16
+  __syncthreads();
+  int rlt = 0, req = 0, tlt = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    const int x = sc.wm[w];
+    rlt += w < wid ? (x & 0xFFFF) : 0;
+    req += w < wid ? (x >> 16) : 0;
+    tlt += x & 0xFFFF;
+  }
+  const int need = k - tlt;  // 1 <= need <= #(key == T)
+  for (int j = 0; j < J; ++j) {
+    const int pos = wbeg + j * 64 + lane;
+    const uint32_t x = pos < n ? (uint32_t)key[pos] : 0u;
+    const bool flt = pos < n && x < T, feq = pos < n && x == T;
+    const uint64_t bl = __builtin_amdgcn_ballot_w64(flt), be = __builtin_amdgcn_ballot_w64(feq);
+    const int lb = rlt + __popcll(bl & lanemask_lt(lane));
+    const int eb = req + __popcll(be & lanemask_lt(lane));
+    if (flt || (feq && eb < need)) {
+      const int r = lb + min(eb, need);
+      if constexpr (TO_LDS) sel[r] = (uint16_t)pos;
+      else out[r] = pos;
+    }
+    rlt += __popcll(bl);
+    req += __popcll(be);
+  }
+}
+
 // Reference-exact selection for one (layer, b, h) row whose zone norms are at `nrow`; working
 // arrays at `arrays` (SelArrays layout for n_cap positions and `cap`-rank windows: LDS, or a
 // global scratch row for zones longer than kZoneMax) and scalars in `sc`; NT threads (the
@@ -1877,7 +2020,7 @@ __device__ __forceinline__ bool select_fast_untied(const KeyT* key, int n, int k
 // int32) or, with TO_LDS, to `sel` (LDS u16, may alias the key region: keys are dead by then).
 // Returns false (and ORs KVC_DEV_SELECT_BOUNDS into *status) when the row exceeds this kernel's
 // zone capacity -- nothing is selected then.
-template <int KC, bool TO_LDS, int MAXN, int NT, bool HH = false>
+template <int KC, bool TO_LDS, int MAXN, int NT, bool HH = false, bool STABLE = false>
 __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, int dt, int order,
                             int algo, const char* __restrict__ nrow, int32_t* out, uint16_t* sel,
                             char* arrays, int n_cap, int cap,
@@ -1982,6 +2125,17 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
   __syncthreads();
   KVC_STAMP(1);
 
+  // ---- KVC_ALGO_STABLE: the first k of a stable sort (ties in position order) ----
+  if constexpr (STABLE) {
+    // the radix histograms (512 ints) over the idx region and the rank tables, unused here
+    // (sel, when in LDS, is the idx region too: written only after the last histogram read);
+    // shorter rows bisect over the key range instead
+    const bool radix = (size_t)n_cap * 2 + (size_t)(cap + 72) * 4 >= 2048;
+    stable_select<NT, KeyT, TO_LDS>(key, n, k, sc, out, sel, reinterpret_cast<int*>(idx), radix);
+    KVC_STAMP(4);
+    return true;
+  }
+
   // ---- reference-exact k-selection ----
   if constexpr (sizeof(KeyT) == 4 && MAXJ <= 16) {  // fp32 keys: untied boundary -> values only
     // (`sel` may alias the key region: the keys are read into registers before any store)
@@ -2079,7 +2233,7 @@ constexpr int kSelBytesBig = (int)sel_bytes(kZoneMax, (int)sizeof(KeyT), kSelCap
 
 // 8 waves per SIMD: two 1024-thread rows per CU (fp32 rows of the big kernel: one per CU, LDS).
 // HH: the heavy-hitter instance (kvc_heavy_hitters), whose heap selects prefilter their scan.
-template <int KC, int NT, bool HH = false>
+template <int KC, int NT, bool HH = false, bool STABLE = false>
 __global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT, HH))
     select_kernel(const LayerChunk T, int BH, int dt, int order, int algo,
                   const char* __restrict__ norms, int64_t norm_stride,
@@ -2094,13 +2248,13 @@ __global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT, HH))
   if constexpr (NT == kSelThreads) {
     // LDS: key[kZoneMax] | idx[kZoneMax] (u16) | spos | gpos (u16 rank windows) -- SelArrays
     __shared__ __attribute__((aligned(16))) char smem[kSelBytesBig<KeyT>];
-    select_body<KC, false, MAXN, NT, HH>(ly, dt, order, algo,
+    select_body<KC, false, MAXN, NT, HH, STABLE>(ly, dt, order, algo,
                                      norms + (int64_t)row * norm_stride * ESZ,
                                      out_idx + (int64_t)row * idx_stride, nullptr, smem, kZoneMax,
                                      kSelCapBig<KeyT>, sc, wave_seg, stamps, status);
   } else {
     extern __shared__ __attribute__((aligned(16))) char dsmem[];
-    select_body<KC, false, MAXN, NT, HH>(ly, dt, order, algo,
+    select_body<KC, false, MAXN, NT, HH, STABLE>(ly, dt, order, algo,
                                      norms + (int64_t)row * norm_stride * ESZ,
                                      out_idx + (int64_t)row * idx_stride, nullptr, dsmem, n_cap,
                                      cap, sc, wave_seg, stamps, status);
@@ -2556,7 +2710,7 @@ __device__ __forceinline__ void gather_row(const kvc_layer_t* __restrict__ ly, i
 // bound), and the index list never round-trips through global memory.  Layout and thread
 // counts as select_kernel; rows without a selection only copy.
 // ---------------------------------------------------------------------------------------------
-template <int KC, int NT, int NC>
+template <int KC, int NT, int NC, bool STABLE = false>
 __global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT))
     select_gather_kernel(const LayerChunk T, int H, int BH, int dt, int order, int algo,
                          const char* __restrict__ norms, int64_t norm_stride, int wave_seg,
@@ -2592,9 +2746,12 @@ __global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT))
     extern __shared__ __attribute__((aligned(16))) char dsmem[];
     arrays = dsmem;
   }
-  uint16_t* sel = reinterpret_cast<uint16_t*>(arrays);  // key region, dead after the chain
+  // the kept positions: over the key region, dead after the chain (the stable selection reads
+  // its keys to the end: the idx region then)
+  uint16_t* sel = reinterpret_cast<uint16_t*>(arrays + (STABLE ? (size_t)n_cap * sizeof(KeyT) : 0));
   if (selects) {
-    const bool ok = select_body<KC, true, MAXN, NT>(ly, dt, order, algo, nrow, nullptr, sel,
+    const bool ok = select_body<KC, true, MAXN, NT, false, STABLE>(ly, dt, order, algo, nrow,
+                                                                  nullptr, sel,
                                                     arrays, n_cap, cap, sc, wave_seg, nullptr,
                                                     status);
     if (!ok) return;  // flagged in *status; the row's output is left unwritten
@@ -2881,7 +3038,8 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
   if (p->dtype != KVC_BF16 && p->dtype != KVC_F16 && p->dtype != KVC_F32) return KVC_E_DTYPE;
   if (p->batch < 1 || p->heads < 1 || p->head_dim < 1) return KVC_E_ARG;
   if (p->order != KVC_ASC && p->order != KVC_DESC) return KVC_E_ARG;
-  if (p->algo != KVC_ALGO_SORT && p->algo != KVC_ALGO_TOPK) return KVC_E_ARG;
+  if (p->algo != KVC_ALGO_SORT && p->algo != KVC_ALGO_TOPK && p->algo != KVC_ALGO_STABLE)
+    return KVC_E_ARG;
   if ((p->flags & ~(KVC_FLAG_SPLIT_SELECT_GATHER | KVC_FLAG_SHARED_INDEX | KVC_FLAG_GATHER_FIXED |
                     KVC_FLAG_GATHER_SELECTED)) || p->reserved != 0)
     return KVC_E_ARG;  // unknown flag bits / reserved field: refuse rather than ignore
@@ -2915,6 +3073,10 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
     if (n_out > 0x7FFFFFFF || 2 * BH * n_out * nc > 0x7FFFFFFF) return KVC_E_ARG;
     const bool needs_select = y.n_select > 0 && y.n_select < y.zone_len;
     if (needs_select && y.zone_len > kZoneMaxLong) return KVC_E_TOO_LONG;
+    // stable selections run from LDS only
+    if (needs_select && p->algo == KVC_ALGO_STABLE && !p->external_index &&
+        y.zone_len > kZoneMax)
+      return KVC_E_TOO_LONG;
     if (n_out > 0) {
       if (!y.k || !y.v || !y.k_out || !y.v_out) return KVC_E_ARG;
       if (!aligned16(y.k) || !aligned16(y.v) || !aligned16(y.k_out) || !aligned16(y.v_out))
@@ -3049,14 +3211,21 @@ static int launch_select(const LayerChunk& T, int cn, int BH, int dt, int order,
                     status);
   }
   const int ks = (int)sizeof(KeyT);
-  if (n_cap <= kSmallZone) {
-    const int cap = sel_cap(n_cap, ks, kSmallBudget);
-    return launch_k(select_kernel<KC, kSelThreadsSmall, HH>, rows_grid, dim3(kSelThreadsSmall),
-                    sel_bytes(n_cap, ks, cap), s, T, BH, dt, order, algo, norms, nstride, idx,
-                    istride, kWaveSegSmall, n_cap, cap, stamps, status);
-  }
-  return launch_k(select_kernel<KC, kSelThreads, HH>, rows_grid, dim3(kSelThreads), 0, s, T, BH, dt,
-                  order, algo, norms, nstride, idx, istride, kWaveSeg, n_cap, 0, stamps, status);
+  const auto go = [&](auto stable) {
+    constexpr bool ST = decltype(stable)::value;
+    if (n_cap <= kSmallZone) {
+      const int cap = sel_cap(n_cap, ks, kSmallBudget);
+      return launch_k(select_kernel<KC, kSelThreadsSmall, HH, ST>, rows_grid,
+                      dim3(kSelThreadsSmall), sel_bytes(n_cap, ks, cap), s, T, BH, dt, order, algo,
+                      norms, nstride, idx, istride, kWaveSegSmall, n_cap, cap, stamps, status);
+    }
+    return launch_k(select_kernel<KC, kSelThreads, HH, ST>, rows_grid, dim3(kSelThreads), 0, s, T,
+                    BH, dt, order, algo, norms, nstride, idx, istride, kWaveSeg, n_cap, 0, stamps,
+                    status);
+  };
+  if constexpr (!HH)
+    if (algo == KVC_ALGO_STABLE) return go(std::true_type());
+  return go(std::false_type());
 }
 
 // One chunk of <= kArgLayers layers: SCORE, then SELECT_GATHER (or SELECT and GATHER as two
@@ -3107,22 +3276,26 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
       const int rows = cn * BH;
       const dim3 rows_grid((unsigned)rows);
       const int ks = (int)sizeof(KeyT);
-      if (n_cap <= kSmallZone) {
-        const int cap = sel_cap(n_cap, ks, kSmallBudget);
-        return launch_k(select_gather_kernel<KC, kSelThreadsSmall, NC>, rows_grid,
-                        dim3(kSelThreadsSmall), sel_bytes(n_cap, ks, cap), s, T, H, BH, DT,
-                        p->order, p->algo, norms, nstride, kWaveSegSmall, n_cap, cap, status, 0);
-      }
-      // fewer rows than CUs (e.g. 4 layers per GPU of an 8-way layer split): one row per CU and
-      // idle CUs -- the sink / tail rows get copy-only workgroups of their own
-      bool fixed = false;
-      for (int l = c0; l < c0 + cn; ++l)
-        fixed |= layer_selects(layers[l]) && layers[l].sink_len + layers[l].tail_len > 0;
-      const int split = fixed && rows <= kSplitCopyRows ? rows : 0;
-      return launch_k(select_gather_kernel<KC, kSelThreads, NC>,
-                      dim3((unsigned)(split ? 2 * rows : rows)), dim3(kSelThreads), 0, s, T, H,
-                      BH, DT, p->order, p->algo, norms, nstride, kWaveSeg, n_cap, 0, status,
-                      split);
+      const auto go = [&](auto stable) {
+        constexpr bool ST = decltype(stable)::value;
+        if (n_cap <= kSmallZone) {
+          const int cap = sel_cap(n_cap, ks, kSmallBudget);
+          return launch_k(select_gather_kernel<KC, kSelThreadsSmall, NC, ST>, rows_grid,
+                          dim3(kSelThreadsSmall), sel_bytes(n_cap, ks, cap), s, T, H, BH, DT,
+                          p->order, p->algo, norms, nstride, kWaveSegSmall, n_cap, cap, status, 0);
+        }
+        // fewer rows than CUs (e.g. 4 layers per GPU of an 8-way layer split): one row per CU
+        // and idle CUs -- the sink / tail rows get copy-only workgroups of their own
+        bool fixed = false;
+        for (int l = c0; l < c0 + cn; ++l)
+          fixed |= layer_selects(layers[l]) && layers[l].sink_len + layers[l].tail_len > 0;
+        const int split = fixed && rows <= kSplitCopyRows ? rows : 0;
+        return launch_k(select_gather_kernel<KC, kSelThreads, NC, ST>,
+                        dim3((unsigned)(split ? 2 * rows : rows)), dim3(kSelThreads), 0, s, T, H,
+                        BH, DT, p->order, p->algo, norms, nstride, kWaveSeg, n_cap, 0, status,
+                        split);
+      };
+      return p->algo == KVC_ALGO_STABLE ? go(std::true_type()) : go(std::false_type());
     }
     char* scratch = w + round_up(info.index_offset + (size_t)info.rows * istride * 4, 256);
     uint64_t* st = stamps ? stamps + (size_t)layers[c0].row0 * 32 : nullptr;
@@ -3145,7 +3318,7 @@ static int debug_select_impl(const kvc_params_t* p, const kvc_layer_t* layers, i
   int rc = plan_impl(p, const_cast<kvc_layer_t*>(layers), nl, &info, false);
   if (rc != KVC_OK) return rc;
   if (nl < 1 || nl > kArgLayers || zone_cap < kTile || zone_cap > kSmallZone ||
-      zone_cap % kTile || p->external_index ||
+      zone_cap % kTile || p->external_index || p->algo == KVC_ALGO_STABLE ||
       (p->phases != KVC_PHASE_SELECT && p->phases != (KVC_PHASE_SELECT | KVC_PHASE_GATHER)))
     return KVC_E_ARG;
   if (!w || wbytes < info.workspace_bytes) return KVC_E_WORKSPACE;

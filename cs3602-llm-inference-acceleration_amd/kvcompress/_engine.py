@@ -157,6 +157,28 @@ _timer = None
 # SCORE, SELECT and GATHER as three kernels (kvc_params.flags KVC_FLAG_SPLIT_SELECT_GATHER).
 split_select_gather = False
 
+# Tie policy of the methods' selections (opt-in; not part of the reference).  "reference"
+# (default): the reference's first-k sets bit-exactly, libstdc++ tie order included.  "stable":
+# tied keys kept in position order -- the first k of argsort(stable=True), for argsort and topk
+# callers alike (KVC_ALGO_STABLE: a radix select, no partition chain).  The two differ only
+# where a tie straddles the k-th key, i.e. on most bf16 / fp16 rows.  KVC_TIE_POLICY=stable in
+# the environment selects it at import, set_tie_policy() at run time.  h2o_attention's
+# heavy hitters keep the reference order either way.
+TIE_POLICIES = ("reference", "stable")
+STABLE_MAX_ZONE = 16384  # kvc.h KVC_ALGO_STABLE: selections run from LDS only
+tie_policy = __import__("os").environ.get("KVC_TIE_POLICY", "reference")
+if tie_policy not in TIE_POLICIES:
+    raise ValueError(f"KVC_TIE_POLICY={tie_policy!r}: expected one of {TIE_POLICIES}")
+
+
+def set_tie_policy(policy: str) -> str:
+    """Select the tie policy ("reference" or "stable") of later calls; returns the previous one."""
+    global tie_policy
+    if policy not in TIE_POLICIES:
+        raise ValueError(f"tie policy {policy!r}: expected one of {TIE_POLICIES}")
+    prev, tie_policy = tie_policy, policy
+    return prev
+
 
 def set_phase_timer(t):
     global _timer
@@ -198,6 +220,14 @@ def _prep(t):
 def execute(jobs: List[Segments], out_list: list, order: int, algo: int):
     if not jobs:
         return
+    if tie_policy == "stable":
+        algo = N.KVC_ALGO_STABLE
+        for j in jobs:
+            if (0 < j.n_select < j.zone_len and j.ext_index is None and
+                    j.zone_len > STABLE_MAX_ZONE):
+                raise ValueError(f"kvcompress: the stable tie policy selects from zones of at most "
+                                 f"{STABLE_MAX_ZONE} positions (layer {j.layer_idx}: "
+                                 f"{j.zone_len}); use the reference policy for longer zones")
     fast = _one_plain_group(jobs)
     if fast is not None:
         _run_plain(*fast, jobs, out_list, order, algo)
@@ -728,7 +758,7 @@ def memoized(fn):
             return fn(kvl, *args, **kwargs)
         try:
             key = (fn, _freeze(args), _freeze(sorted(kwargs.items())), split_select_gather,
-                   torch.cuda.current_stream(sig[4]).cuda_stream, sig)
+                   tie_policy, torch.cuda.current_stream(sig[4]).cuda_stream, sig)
         except TypeError:
             return fn(kvl, *args, **kwargs)
         rec = call_memo.get(key)
@@ -738,10 +768,10 @@ def memoized(fn):
                 with torch.cuda.device(sig[4]):
                     return hm.run(kvl, rec.actions, rec.table, rec.n_jobs, rec.n_outs,
                                   ctypes_addr(rec.params), rec.ws.data_ptr(), rec.ws_bytes,
-                                  key[4])
+                                  key[5])
             return hm.run(kvl, rec.actions, rec.table, rec.n_jobs, rec.n_outs,
                           ctypes_addr(rec.params) if rec.n_jobs else 0,
-                          rec.ws.data_ptr() if rec.n_jobs else 0, rec.ws_bytes, key[4])
+                          rec.ws.data_ptr() if rec.n_jobs else 0, rec.ws_bytes, key[5])
         if not call_memo.admit(key):
             return fn(kvl, *args, **kwargs)
         _recording = []
@@ -751,7 +781,7 @@ def memoized(fn):
         finally:
             _recording = None
         rec = _record(kvl, out, launches)
-        if rec is not None and all(l[0] == key[4] for l in launches):
+        if rec is not None and all(l[0] == key[5] for l in launches):
             call_memo.put(key, rec, rec.ws_bytes)
             memo_stats["recorded"] += 1
         return out

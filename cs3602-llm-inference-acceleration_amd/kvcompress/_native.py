@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("KVC_LIB", LIB_PATH)
 
 KVC_F32, KVC_BF16, KVC_F16 = 0, 1, 2
 KVC_ASC, KVC_DESC = 0, 1
-KVC_ALGO_SORT, KVC_ALGO_TOPK = 0, 1
+KVC_ALGO_SORT, KVC_ALGO_TOPK, KVC_ALGO_STABLE = 0, 1, 2
 KVC_SCORE_NORM, KVC_SCORE_SNAPKV = 0, 1
 PHASE_SCORE, PHASE_SELECT, PHASE_GATHER, PHASE_ALL = 1, 2, 4, 7
 FLAG_SPLIT_SELECT_GATHER, FLAG_SHARED_INDEX, FLAG_GATHER_FIXED, FLAG_GATHER_SELECTED = 1, 2, 4, 8

@@ -60,8 +60,12 @@ enum kvc_dtype { KVC_F32 = 0, KVC_BF16 = 1, KVC_F16 = 2 };
 enum kvc_order { KVC_ASC = 0, KVC_DESC = 1 };
 /* KVC_ALGO_SORT: set of argsort(stable=False)[:k] = libstdc++ std::sort (introsort)
  * KVC_ALGO_TOPK: set of torch.topk = std::nth_element (introselect), or std::partial_sort
- *                (heap select) when k*64 <= n, exactly as aten TopKImpl.h chooses. */
-enum kvc_algo { KVC_ALGO_SORT = 0, KVC_ALGO_TOPK = 1 };
+ *                (heap select) when k*64 <= n, exactly as aten TopKImpl.h chooses.
+ * KVC_ALGO_STABLE (opt-in, not the reference's tie order): set of argsort(stable=True)[:k] --
+ *                every key strictly before the k-th one and the first of the tied keys in
+ *                position order; the same set for sort and topk callers.  A radix select with
+ *                no partition chain.  Zones of at most 16 384 positions (else KVC_E_TOO_LONG). */
+enum kvc_algo { KVC_ALGO_SORT = 0, KVC_ALGO_TOPK = 1, KVC_ALGO_STABLE = 2 };
 enum kvc_score { KVC_SCORE_NORM = 0, KVC_SCORE_SNAPKV = 1 };
 enum kvc_phase {
   KVC_PHASE_SCORE = 1,

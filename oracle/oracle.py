@@ -27,6 +27,12 @@ _LIB = None
 
 DT_F32, DT_BF16, DT_F16 = 0, 1, 2
 
+# Tie policy of argsort_prefix / topk_indices: "reference" (libstdc++ std::sort / nth_element /
+# partial_sort, the reference's order) or "stable" (the engine's opt-in KVC_ALGO_STABLE: the
+# first k of torch.argsort(stable=True), ties in position order; pinned against torch by
+# tests/test_stable_ties.py).
+TIE = "reference"
+
 
 def lib():
     global _LIB
@@ -74,8 +80,31 @@ def norms(K):
     return out
 
 
+def as_float(vals):
+    """Values of a bf16 (uint16 bits) / fp16 / fp32 array as float32 (exact)."""
+    if vals.dtype == np.uint16:
+        return (vals.astype(np.uint32) << 16).view(np.float32)
+    return vals.astype(np.float32)
+
+
+def stable_prefix(vals, k, descending=False):
+    """The first k of a stable sort along the last axis (NaN last ascending, first descending,
+    as torch.sort orders them), in sort order."""
+    v = as_float(np.ascontiguousarray(vals))
+    nan = np.isnan(v)
+    B, H, n = v.shape
+    out = np.empty((B, H, k), dtype=np.int64)
+    for b in range(B):
+        for h in range(H):
+            keys = (-v[b, h], ~nan[b, h]) if descending else (v[b, h], nan[b, h])
+            out[b, h] = np.lexsort(keys)[:k]
+    return out
+
+
 def argsort_prefix(vals, k, descending=False):
     """vals.argsort(dim=-1, descending)[..., :k] (k >= 0) in sort order."""
+    if TIE == "stable":
+        return stable_prefix(vals, k, descending)
     vals = np.ascontiguousarray(vals)
     B, H, n = vals.shape
     out = np.empty((B, H, k), dtype=np.int64)
@@ -90,6 +119,8 @@ def argsort_prefix(vals, k, descending=False):
 
 def topk_indices(vals, k):
     """torch.topk(vals, k, dim=-1)[1] (largest=True, sorted=True)."""
+    if TIE == "stable":
+        return stable_prefix(vals, k, descending=True)
     vals = np.ascontiguousarray(vals)
     B, H, n = vals.shape
     out = np.empty((B, H, k), dtype=np.int64)
