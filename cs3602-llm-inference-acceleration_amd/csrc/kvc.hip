@@ -1872,25 +1872,30 @@ __device__ __forceinline__ bool select_fast_untied(const KeyT* key, int n, int k
 
 // KVC_ALGO_STABLE (opt-in, not the reference's tie order): the first k of a STABLE sort of the
 // row's keys -- every key below T, the k-th smallest key, then the first k - #(key < T) keys
-// equal to T in position order.  T by the radix select of select_fast_untied (8-bit digits of
-// key - min from the top, a 256-bin LDS histogram per digit in `hist`, 512 ints) or, for rows
-// whose scratch is shorter, by bisection over the key range; then one counting pass and the
-// ascending emission (output slot of a kept position = #(key < T before it) + min(#(key == T
-// before it), need)).  The keys stay in LDS (read once per pass, nothing held in registers);
-// `sel` must not alias them.
-template <int NT, typename KeyT, bool TO_LDS>
+// equal to T in position order.  T by a radix select (8-bit digits of key - min from the top, a
+// 256-bin LDS histogram per digit in `hist`, 512 ints: one digit for a bf16 norm row, whose keys
+// span < 256 codes) or, for rows whose scratch is shorter, by bisection over the key range; then
+// one flag pass and the ascending emission (output slot of a kept position = #(key < T before
+// it) + min(#(key == T before it), need)).  Lane positions wid*J*64 + j*64 + lane, j < J <= JM:
+// every pass re-reads the keys from LDS with its JM loads issued back to back (nothing but two
+// flag words held across barriers).  `sel` must not alias the keys.
+template <int NT, int JM, typename KeyT, bool TO_LDS>
 __device__ __forceinline__ void stable_select(const KeyT* key, int n, int k, SelScalars<KeyT>& sc,
-                                              int32_t* out, uint16_t* sel, int* hist, bool radix) {
+                                              int32_t* out, uint16_t* sel, int* hist, bool radix,
+                                              uint64_t* stamps = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wid = (NT == 64) ? 0 : uni(tid >> 6);
-  const int J = (n + NT - 1) / NT;  // positions wid*J*64 + j*64 + lane, j < J, per wave
-  const int wbeg = wid * J * 64;
+  const int J = (n + NT - 1) / NT;
+  const int base = wid * J * 64 + lane;
+  const int jv = base < n ? min(J, (n - base + 63) >> 6) : 0;  // this lane's valid j
   uint32_t mn = 0xFFFFFFFFu, mx = 0u;
-  for (int j = 0; j < J; ++j) {
-    const int pos = wbeg + j * 64 + lane;
-    if (pos < n) {
-      const uint32_t x = (uint32_t)key[pos];
-      mn = min(mn, x);
-      mx = max(mx, x);
+  {
+    uint32_t x[JM];
+#pragma unroll
+    for (int j = 0; j < JM; ++j) x[j] = j < jv ? (uint32_t)key[base + j * 64] : 0u;
+#pragma unroll
+    for (int j = 0; j < JM; ++j) {
+      mn = j < jv ? min(mn, x[j]) : mn;
+      mx = j < jv ? max(mx, x[j]) : mx;
     }
   }
 #pragma unroll
@@ -1902,6 +1907,8 @@ __device__ __forceinline__ void stable_select(const KeyT* key, int n, int k, Sel
     sc.wa[wid] = (int)mn;
     sc.wb[wid] = (int)mx;
   }
+  if (radix)
+    for (int i = tid; i < 512; i += NT) hist[i] = 0;
   __syncthreads();
   uint32_t lo = 0xFFFFFFFFu, hi = 0u;
 #pragma unroll
@@ -1911,25 +1918,28 @@ __device__ __forceinline__ void stable_select(const KeyT* key, int n, int k, Sel
   }
   lo = (uint32_t)uni((int)lo);
   hi = (uint32_t)uni((int)hi);
-  __syncthreads();  // sc.wa / sc.wb are reused below
+  KVC_STAMP(2);
   int parity = 0;
   if (radix) {
+    // the first pass publishes in sc.wa[1] / sc.wb[1], the next in [2] ... (read after its
+    // barrier; no slot is rewritten), so the min / max words above may still be being read
     int rem = hi - lo ? 32 - __builtin_clz(hi - lo) : 0;  // offset bits still undecided
     uint32_t prefix = 0;
-    int below = 0;
-    for (int i = tid; i < 512; i += NT) hist[i] = 0;
-    __syncthreads();
+    int below = 0, slot = 1;
     while (rem > 0) {
       const int w = min(8, rem), sh = rem - w;
       int* h = hist + 256 * parity;
-      for (int j = 0; j < J; ++j) {
-        const int pos = wbeg + j * 64 + lane;
-        if (pos < n) {
-          const uint32_t d = (uint32_t)key[pos] - lo;
-          if ((uint32_t)((uint64_t)d >> rem) == prefix) lds_add1(h + ((d >> sh) & ((1u << w) - 1u)));
-        }
+      uint32_t x[JM];
+#pragma unroll
+      for (int j = 0; j < JM; ++j) x[j] = j < jv ? (uint32_t)key[base + j * 64] : 0u;
+#pragma unroll
+      for (int j = 0; j < JM; ++j) {
+        const uint32_t d = x[j] - lo;
+        if (j < jv && (rem == 32 ? 0u : d >> rem) == prefix)
+          lds_add1(h + ((d >> sh) & ((1u << w) - 1u)));
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // the other buffer's last reader (wave 0, previous pass) finished before the last barrier
       for (int i = tid; i < 256; i += NT) hist[256 * (parity ^ 1) + i] = 0;
       __syncthreads();
       if (wid == 0) {
@@ -1948,27 +1958,30 @@ __device__ __forceinline__ void stable_select(const KeyT* key, int n, int k, Sel
               if (c + c2 < need) { c += c2; ++bin; }
             }
           }
-          sc.wa[0] = bin;
-          sc.wb[0] = below + c;
+          sc.wa[slot] = bin;
+          sc.wb[slot] = below + c;
         }
       }
       __syncthreads();
-      prefix = (prefix << w) | (uint32_t)sc.wa[0];
-      below = sc.wb[0];
+      prefix = (prefix << w) | (uint32_t)sc.wa[slot];
+      below = sc.wb[slot];
+      ++slot;  // <= 4 passes: slots 1..4 of 16
       rem = sh;
       parity ^= 1;
-      __syncthreads();  // sc.wa[0] / sc.wb[0] are rewritten by the next pass
     }
     lo = lo + prefix;
+  } else {
+    __syncthreads();  // sc.wa / sc.wb are the bisection's count buffers
   }
-  // smallest v with #(key <= v) >= k (bisection; the radix select leaves lo == hi's answer)
+  // smallest v with #(key <= v) >= k (bisection; the radix select leaves lo at it)
   while (!radix && lo < hi) {
     const uint32_t mid = lo + ((hi - lo) >> 1);
+    uint32_t x[JM];
+#pragma unroll
+    for (int j = 0; j < JM; ++j) x[j] = j < jv ? (uint32_t)key[base + j * 64] : 0u;
     int cl = 0;
-    for (int j = 0; j < J; ++j) {
-      const int pos = wbeg + j * 64 + lane;
-      cl += (pos < n && (uint32_t)key[pos] <= mid) ? 1 : 0;
-    }
+#pragma unroll
+    for (int j = 0; j < JM; ++j) cl += (j < jv && x[j] <= mid) ? 1 : 0;
     const int rs = row_scan16(cl);
     const int c = __builtin_amdgcn_readlane(rs, 15) + __builtin_amdgcn_readlane(rs, 31) +
                   __builtin_amdgcn_readlane(rs, 47) + __builtin_amdgcn_readlane(rs, 63);
@@ -1977,13 +1990,22 @@ __device__ __forceinline__ void stable_select(const KeyT* key, int n, int k, Sel
     if (tot >= k) hi = mid;
     else lo = mid + 1;
   }
+  KVC_STAMP(3);
   const uint32_t T = lo;
+  uint32_t ltm = 0, eqm = 0;  // this lane's flags by j
   int clt = 0, ceq = 0;
-  for (int j = 0; j < J; ++j) {
-    const int pos = wbeg + j * 64 + lane;
-    const uint32_t x = pos < n ? (uint32_t)key[pos] : 0u;
-    clt += __popcll(__builtin_amdgcn_ballot_w64(pos < n && x < T));
-    ceq += __popcll(__builtin_amdgcn_ballot_w64(pos < n && x == T));
+  {
+    uint32_t x[JM];
+#pragma unroll
+    for (int j = 0; j < JM; ++j) x[j] = j < jv ? (uint32_t)key[base + j * 64] : 0u;
+#pragma unroll
+    for (int j = 0; j < JM; ++j) {
+      const bool flt = j < jv && x[j] < T, feq = j < jv && x[j] == T;
+      ltm |= flt ? 1u << j : 0u;
+      eqm |= feq ? 1u << j : 0u;
+      clt += __popcll(__builtin_amdgcn_ballot_w64(flt));
+      ceq += __popcll(__builtin_amdgcn_ballot_w64(feq));
+    }
   }
   if (lane == 0) sc.wm[wid] = clt | (ceq << 16);  // each <= kZoneMax < 2^16
   __syncthreads();
@@ -1996,17 +2018,16 @@ __device__ __forceinline__ void stable_select(const KeyT* key, int n, int k, Sel
     tlt += x & 0xFFFF;
   }
   const int need = k - tlt;  // 1 <= need <= #(key == T)
-  for (int j = 0; j < J; ++j) {
-    const int pos = wbeg + j * 64 + lane;
-    const uint32_t x = pos < n ? (uint32_t)key[pos] : 0u;
-    const bool flt = pos < n && x < T, feq = pos < n && x == T;
+#pragma unroll
+  for (int j = 0; j < JM; ++j) {
+    const bool flt = (ltm >> j) & 1u, feq = (eqm >> j) & 1u;
     const uint64_t bl = __builtin_amdgcn_ballot_w64(flt), be = __builtin_amdgcn_ballot_w64(feq);
     const int lb = rlt + __popcll(bl & lanemask_lt(lane));
     const int eb = req + __popcll(be & lanemask_lt(lane));
     if (flt || (feq && eb < need)) {
       const int r = lb + min(eb, need);
-      if constexpr (TO_LDS) sel[r] = (uint16_t)pos;
-      else out[r] = pos;
+      if constexpr (TO_LDS) sel[r] = (uint16_t)(base + j * 64);
+      else out[r] = base + j * 64;
     }
     rlt += __popcll(bl);
     req += __popcll(be);
@@ -2127,11 +2148,13 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
 
   // ---- KVC_ALGO_STABLE: the first k of a stable sort (ties in position order) ----
   if constexpr (STABLE) {
+    static_assert(MAXJ <= 16, "stable selection: positions per lane (flag words)");
     // the radix histograms (512 ints) over the idx region and the rank tables, unused here
     // (sel, when in LDS, is the idx region too: written only after the last histogram read);
     // shorter rows bisect over the key range instead
     const bool radix = (size_t)n_cap * 2 + (size_t)(cap + 72) * 4 >= 2048;
-    stable_select<NT, KeyT, TO_LDS>(key, n, k, sc, out, sel, reinterpret_cast<int*>(idx), radix);
+    stable_select<NT, MAXJ, KeyT, TO_LDS>(key, n, k, sc, out, sel, reinterpret_cast<int*>(idx),
+                                          radix, stamps);
     KVC_STAMP(4);
     return true;
   }

@@ -51,6 +51,14 @@ for rep in range(3):
 rows = int(info.rows)
 allst = ws[-rows * 256:].view(torch.int64).view(rows, 32).cpu().numpy().astype(np.float64)
 st = allst[:, :5]
+if ALGO == 2:  # KVC_ALGO_STABLE: key load | min/max | radix (or bisection) | count + emission
+    d = np.diff(st, axis=1)
+    res["median_cycles"] = {n: float(np.median(d[:, i])) for i, n in enumerate(
+        ("key_load", "min_max", "radix", "count_emit"))}
+    res["row_total_median"] = float(np.median(st[:, 4] - st[:, 0]))
+    res["span_cycles"] = float(st[:, 4].max() - st[:, 0].min())
+    print(json.dumps(res))
+    sys.exit(0)
 for nm, off in (("block", 5), ("wave", 10)):
     acc = allst[:, off:off + 5]
     res[nm + "_levels_median"] = float(np.median(acc[:, 3]))
