@@ -100,7 +100,8 @@ enum kvc_status {
   KVC_E_DTYPE = -2,     /* dtype is not bf16 / fp16 / fp32                            */
   KVC_E_HEADDIM = -3,   /* head_dim*elem_size not in {64,128,160,256,320,512,1024} B  */
   KVC_E_ALIGN = -4,     /* a base pointer or stride is not 16-byte aligned            */
-  KVC_E_TOO_LONG = -5,  /* a scored zone is longer than kvc_max_zone_len() (2^24)     */
+  KVC_E_TOO_LONG = -5,  /* a scored zone is longer than kvc_max_zone_len() (2^24), or a
+                           KVC_ALGO_STABLE selection zone longer than 16 384            */
   KVC_E_WORKSPACE = -6, /* workspace smaller than kvc_plan() reported                 */
   KVC_E_HIP = -7        /* a HIP launch failed                                        */
 };

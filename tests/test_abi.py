@@ -241,3 +241,22 @@ def test_attn_accumulate_validates_before_launching():
     bad[0]["q_len"] = 0
     assert N.attn_accumulate(_attn_params(), bad, 0) == -1
     assert N.attn_accumulate(_attn_params(batch=0), t, 0) == -1
+
+
+def test_algo_enum_and_stable_zone_limit():
+    """kvc_algo in the header equals the Python constants; kvc_plan accepts KVC_ALGO_STABLE for
+    zones up to 16 384 positions (KVC_E_TOO_LONG beyond, unless the indices are external) and
+    refuses unknown algorithms."""
+    src = open(os.path.join(ROOT, "include", "kvc.h")).read()
+    enum = re.search(r"enum kvc_algo \{([^}]*)\}", src).group(1)
+    vals = dict((a.strip(), int(b)) for a, b in re.findall(r"(\w+)\s*=\s*(\d+)", enum))
+    assert vals == {"KVC_ALGO_SORT": N.KVC_ALGO_SORT, "KVC_ALGO_TOPK": N.KVC_ALGO_TOPK,
+                    "KVC_ALGO_STABLE": N.KVC_ALGO_STABLE}
+    ok = np.array([_layer(16384, 0, 16384, 512)], dtype=N.LAYER_DTYPE)
+    assert N.plan(_params(algo=N.KVC_ALGO_STABLE), ok)[0] == 0
+    long = np.array([_layer(16448, 0, 16448, 512)], dtype=N.LAYER_DTYPE)
+    assert N.plan(_params(algo=N.KVC_ALGO_STABLE), long.copy())[0] == N.KVC_E_TOO_LONG
+    assert N.plan(_params(algo=N.KVC_ALGO_SORT), long.copy())[0] == 0
+    assert N.plan(_params(algo=N.KVC_ALGO_STABLE, external_index=1,
+                          phases=N.PHASE_GATHER), long.copy())[0] == 0
+    assert N.plan(_params(algo=3), ok.copy())[0] == -1  # KVC_E_ARG
