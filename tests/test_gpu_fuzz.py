@@ -40,12 +40,8 @@ def _kwargs(rng, method, S):
     return dict(window_size=r(1, S))  # recent_only
 
 
-@pytest.mark.parametrize("case", range(N_CASES))
-def test_random_configs_match_oracle(case, monkeypatch):
-    from kvcompress.methods import get_compress_fn
-    # launch paths in rotation: SCORE + SELECT_GATHER, and SCORE / SELECT / GATHER
-    from kvcompress import _engine
-    monkeypatch.setattr(_engine, "split_select_gather", case % 2 == 1)
+def _gen_case(case, max_len=None):
+    """Seeded (method, layers, kwargs) of one fuzz case (layer lengths clipped to max_len)."""
     rng = np.random.default_rng(90000 + case)
     method = str(rng.choice(["fix_size_l2", "l2_compress", "streaming_llm", "h2o_l2",
                              "snapkv_lite", "pyramid_kv", "adaptive_l2", "recent_only"]))
@@ -58,6 +54,8 @@ def test_random_configs_match_oracle(case, monkeypatch):
     layers = []
     for li in range(n_layers):
         S = max(1, S0 + int(rng.integers(-S0 // 4, S0 // 4 + 1)))
+        if max_len:
+            S = min(S, max_len)
         shape = (B, H, S, D)
         seed = 100000 + 100 * case + li
         layers.append((prng.gen_keys(seed, shape, dtype, str(rng.choice(variants))),
@@ -65,6 +63,11 @@ def test_random_configs_match_oracle(case, monkeypatch):
     kw = _kwargs(rng, method, S0)
     kw["skip_layers"] = [int(x) for x in rng.choice(n_layers, size=int(rng.integers(0, 2)),
                                                       replace=False)]
+    return method, layers, kw, dtype, D
+
+
+def _check(case, method, layers, kw, dtype, D):
+    from kvcompress.methods import get_compress_fn
     try:
         ref = oracle.METHODS[method](layers, **kw)
     except Exception as e:  # the reference raises here too (same shape rules)
@@ -79,3 +82,23 @@ def test_random_configs_match_oracle(case, monkeypatch):
         assert kind_of(ki, ko) == kind, ctx
         assert np.array_equal(to_np(ko).view(np.uint8), np.ascontiguousarray(rk).view(np.uint8)), ctx
         assert np.array_equal(to_np(vo).view(np.uint8), np.ascontiguousarray(rv).view(np.uint8)), ctx
+
+
+@pytest.mark.parametrize("case", range(N_CASES))
+def test_random_configs_match_oracle(case, monkeypatch):
+    # launch paths in rotation: SCORE + SELECT_GATHER, and SCORE / SELECT / GATHER
+    from kvcompress import _engine
+    monkeypatch.setattr(_engine, "split_select_gather", case % 2 == 1)
+    _check(case, *_gen_case(case))
+
+
+@pytest.mark.parametrize("case", range(N_CASES // 3))
+def test_random_configs_stable_policy_match_oracle(case, monkeypatch):
+    """The same generator under the opt-in stable tie policy (engine and oracle alike); layers
+    of at most 16 384 positions (the policy's limit)."""
+    from kvcompress import _engine
+    monkeypatch.setattr(_engine, "split_select_gather", case % 2 == 0)
+    monkeypatch.setattr(_engine, "tie_policy", "stable")
+    monkeypatch.setattr(oracle, "TIE", "stable")
+    _engine.call_memo.clear()
+    _check(case, *_gen_case(case, max_len=16384))
