@@ -1887,15 +1887,17 @@ __device__ __forceinline__ void stable_select(const KeyT* key, int n, int k, Sel
   const int J = (n + NT - 1) / NT;
   const int base = wid * J * 64 + lane;
   const int jv = base < n ? min(J, (n - base + 63) >> 6) : 0;  // this lane's valid j
+  constexpr int CH = JM < 16 ? JM : 16;  // loads issued together per pass step
   uint32_t mn = 0xFFFFFFFFu, mx = 0u;
-  {
-    uint32_t x[JM];
 #pragma unroll
-    for (int j = 0; j < JM; ++j) x[j] = j < jv ? (uint32_t)key[base + j * 64] : 0u;
+  for (int j0 = 0; j0 < JM; j0 += CH) {
+    uint32_t x[CH];
 #pragma unroll
-    for (int j = 0; j < JM; ++j) {
-      mn = j < jv ? min(mn, x[j]) : mn;
-      mx = j < jv ? max(mx, x[j]) : mx;
+    for (int j = 0; j < CH; ++j) x[j] = j0 + j < jv ? (uint32_t)key[base + (j0 + j) * 64] : 0u;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      mn = j0 + j < jv ? min(mn, x[j]) : mn;
+      mx = j0 + j < jv ? max(mx, x[j]) : mx;
     }
   }
 #pragma unroll
@@ -1929,14 +1931,17 @@ __device__ __forceinline__ void stable_select(const KeyT* key, int n, int k, Sel
     while (rem > 0) {
       const int w = min(8, rem), sh = rem - w;
       int* h = hist + 256 * parity;
-      uint32_t x[JM];
 #pragma unroll
-      for (int j = 0; j < JM; ++j) x[j] = j < jv ? (uint32_t)key[base + j * 64] : 0u;
+      for (int j0 = 0; j0 < JM; j0 += CH) {
+        uint32_t x[CH];
 #pragma unroll
-      for (int j = 0; j < JM; ++j) {
-        const uint32_t d = x[j] - lo;
-        if (j < jv && (rem == 32 ? 0u : d >> rem) == prefix)
-          lds_add1(h + ((d >> sh) & ((1u << w) - 1u)));
+        for (int j = 0; j < CH; ++j) x[j] = j0 + j < jv ? (uint32_t)key[base + (j0 + j) * 64] : 0u;
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+          const uint32_t d = x[j] - lo;
+          if (j0 + j < jv && (rem == 32 ? 0u : d >> rem) == prefix)
+            lds_add1(h + ((d >> sh) & ((1u << w) - 1u)));
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       // the other buffer's last reader (wave 0, previous pass) finished before the last barrier
@@ -1976,12 +1981,15 @@ __device__ __forceinline__ void stable_select(const KeyT* key, int n, int k, Sel
   // smallest v with #(key <= v) >= k (bisection; the radix select leaves lo at it)
   while (!radix && lo < hi) {
     const uint32_t mid = lo + ((hi - lo) >> 1);
-    uint32_t x[JM];
-#pragma unroll
-    for (int j = 0; j < JM; ++j) x[j] = j < jv ? (uint32_t)key[base + j * 64] : 0u;
     int cl = 0;
 #pragma unroll
-    for (int j = 0; j < JM; ++j) cl += (j < jv && x[j] <= mid) ? 1 : 0;
+    for (int j0 = 0; j0 < JM; j0 += CH) {
+      uint32_t x[CH];
+#pragma unroll
+      for (int j = 0; j < CH; ++j) x[j] = j0 + j < jv ? (uint32_t)key[base + (j0 + j) * 64] : 0u;
+#pragma unroll
+      for (int j = 0; j < CH; ++j) cl += (j0 + j < jv && x[j] <= mid) ? 1 : 0;
+    }
     const int rs = row_scan16(cl);
     const int c = __builtin_amdgcn_readlane(rs, 15) + __builtin_amdgcn_readlane(rs, 31) +
                   __builtin_amdgcn_readlane(rs, 47) + __builtin_amdgcn_readlane(rs, 63);
@@ -1992,17 +2000,19 @@ __device__ __forceinline__ void stable_select(const KeyT* key, int n, int k, Sel
   }
   KVC_STAMP(3);
   const uint32_t T = lo;
-  uint32_t ltm = 0, eqm = 0;  // this lane's flags by j
+  typedef typename std::conditional<(JM > 32), uint64_t, uint32_t>::type FlagT;
+  FlagT ltm = 0, eqm = 0;  // this lane's flags by j
   int clt = 0, ceq = 0;
-  {
-    uint32_t x[JM];
 #pragma unroll
-    for (int j = 0; j < JM; ++j) x[j] = j < jv ? (uint32_t)key[base + j * 64] : 0u;
+  for (int j0 = 0; j0 < JM; j0 += CH) {
+    uint32_t x[CH];
 #pragma unroll
-    for (int j = 0; j < JM; ++j) {
-      const bool flt = j < jv && x[j] < T, feq = j < jv && x[j] == T;
-      ltm |= flt ? 1u << j : 0u;
-      eqm |= feq ? 1u << j : 0u;
+    for (int j = 0; j < CH; ++j) x[j] = j0 + j < jv ? (uint32_t)key[base + (j0 + j) * 64] : 0u;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const bool flt = j0 + j < jv && x[j] < T, feq = j0 + j < jv && x[j] == T;
+      ltm |= flt ? (FlagT)1 << (j0 + j) : (FlagT)0;
+      eqm |= feq ? (FlagT)1 << (j0 + j) : (FlagT)0;
       clt += __popcll(__builtin_amdgcn_ballot_w64(flt));
       ceq += __popcll(__builtin_amdgcn_ballot_w64(feq));
     }
@@ -2148,13 +2158,19 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
 
   // ---- KVC_ALGO_STABLE: the first k of a stable sort (ties in position order) ----
   if constexpr (STABLE) {
-    static_assert(MAXJ <= 16, "stable selection: positions per lane (flag words)");
-    // the radix histograms (512 ints) over the idx region and the rank tables, unused here
-    // (sel, when in LDS, is the idx region too: written only after the last histogram read);
-    // shorter rows bisect over the key range instead
-    const bool radix = (size_t)n_cap * 2 + (size_t)(cap + 72) * 4 >= 2048;
-    stable_select<NT, MAXJ, KeyT, TO_LDS>(key, n, k, sc, out, sel, reinterpret_cast<int*>(idx),
-                                          radix, stamps);
+    static_assert(MAXJ <= 64, "stable selection: positions per lane (flag words)");
+    if constexpr (MAXN > kZoneMax) {
+      // the global-scratch variant (zones up to kZoneMaxGlobal): the histograms in LDS
+      __shared__ int stable_hist[512];
+      stable_select<NT, MAXJ, KeyT, TO_LDS>(key, n, k, sc, out, sel, stable_hist, true, stamps);
+    } else {
+      // the radix histograms (512 ints) over the idx region and the rank tables, unused here
+      // (sel, when in LDS, is the idx region too: written only after the last histogram read);
+      // shorter rows bisect over the key range instead
+      const bool radix = (size_t)n_cap * 2 + (size_t)(cap + 72) * 4 >= 2048;
+      stable_select<NT, MAXJ, KeyT, TO_LDS>(key, n, k, sc, out, sel, reinterpret_cast<int*>(idx),
+                                            radix, stamps);
+    }
     KVC_STAMP(4);
     return true;
   }
@@ -2287,7 +2303,7 @@ __global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT, HH))
 // Zones longer than kZoneMax (up to kZoneMaxGlobal): the same selection with its arrays in a
 // per-row global scratch (L2 / Infinity-Cache resident; a workgroup barrier orders the
 // workgroup's global accesses like LDS ones -- all its waves share one CU's L1).
-template <int KC>
+template <int KC, bool STABLE = false>
 __global__ void __launch_bounds__(kSelThreads)
     select_global_kernel(const LayerChunk T, int BH, int dt, int order, int algo,
                          const char* __restrict__ norms, int64_t norm_stride,
@@ -2299,7 +2315,7 @@ __global__ void __launch_bounds__(kSelThreads)
   __shared__ SelScalars<KeyT> sc;
   const kvc_layer_t* ly = T.l + blockIdx.x / BH;
   const int row = ly->row0 + (int)(blockIdx.x % BH);
-  select_body<KC, false, kZoneMaxGlobal, kSelThreads>(
+  select_body<KC, false, kZoneMaxGlobal, kSelThreads, false, STABLE>(
       ly, dt, order, algo, norms + (int64_t)row * norm_stride * ESZ,
       out_idx + (int64_t)row * idx_stride, nullptr, scratch + (int64_t)row * scratch_row_bytes,
       n_cap, n_cap / 2 + 1, sc, wave_seg, nullptr, status);
@@ -3096,9 +3112,9 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
     if (n_out > 0x7FFFFFFF || 2 * BH * n_out * nc > 0x7FFFFFFF) return KVC_E_ARG;
     const bool needs_select = y.n_select > 0 && y.n_select < y.zone_len;
     if (needs_select && y.zone_len > kZoneMaxLong) return KVC_E_TOO_LONG;
-    // stable selections run from LDS only
+    // stable selections: LDS, or the u16-position global scratch (not the u32 long variant)
     if (needs_select && p->algo == KVC_ALGO_STABLE && !p->external_index &&
-        y.zone_len > kZoneMax)
+        y.zone_len > kZoneMaxGlobal)
       return KVC_E_TOO_LONG;
     if (n_out > 0) {
       if (!y.k || !y.v || !y.k_out || !y.v_out) return KVC_E_ARG;
@@ -3229,6 +3245,11 @@ static int launch_select(const LayerChunk& T, int cn, int BH, int dt, int order,
     if (n_cap > kZoneMaxGlobal)  // u32 positions (the call's longest zone decides)
       return launch_k(select_long_kernel<KC>, rows_grid, dim3(kSelThreads), 0, s, T, BH, dt,
                       order, algo, norms, nstride, idx, istride, scratch, rb, n_cap, status);
+    if constexpr (!HH)
+      if (algo == KVC_ALGO_STABLE)
+        return launch_k(select_global_kernel<KC, true>, rows_grid, dim3(kSelThreads), 0, s, T, BH,
+                        dt, order, algo, norms, nstride, idx, istride, kWaveSeg, scratch, rb,
+                        n_cap, status);
     return launch_k(select_global_kernel<KC>, rows_grid, dim3(kSelThreads), 0, s, T, BH, dt,
                     order, algo, norms, nstride, idx, istride, kWaveSeg, scratch, rb, n_cap,
                     status);

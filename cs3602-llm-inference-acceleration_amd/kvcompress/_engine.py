@@ -165,7 +165,7 @@ split_select_gather = False
 # the environment selects it at import, set_tie_policy() at run time.  h2o_attention's
 # heavy hitters keep the reference order either way.
 TIE_POLICIES = ("reference", "stable")
-STABLE_MAX_ZONE = 16384  # kvc.h KVC_ALGO_STABLE: selections run from LDS only
+STABLE_MAX_ZONE = 65536  # kvc.h KVC_ALGO_STABLE: the LDS and u16-position global kernels
 tie_policy = __import__("os").environ.get("KVC_TIE_POLICY", "reference")
 if tie_policy not in TIE_POLICIES:
     raise ValueError(f"KVC_TIE_POLICY={tie_policy!r}: expected one of {TIE_POLICIES}")

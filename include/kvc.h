@@ -64,7 +64,7 @@ enum kvc_order { KVC_ASC = 0, KVC_DESC = 1 };
  * KVC_ALGO_STABLE (opt-in, not the reference's tie order): set of argsort(stable=True)[:k] --
  *                every key strictly before the k-th one and the first of the tied keys in
  *                position order; the same set for sort and topk callers.  A radix select with
- *                no partition chain.  Zones of at most 16 384 positions (else KVC_E_TOO_LONG). */
+ *                no partition chain.  Zones of at most 65 536 positions (else KVC_E_TOO_LONG). */
 enum kvc_algo { KVC_ALGO_SORT = 0, KVC_ALGO_TOPK = 1, KVC_ALGO_STABLE = 2 };
 enum kvc_score { KVC_SCORE_NORM = 0, KVC_SCORE_SNAPKV = 1 };
 enum kvc_phase {
@@ -101,7 +101,7 @@ enum kvc_status {
   KVC_E_HEADDIM = -3,   /* head_dim*elem_size not in {64,128,160,256,320,512,1024} B  */
   KVC_E_ALIGN = -4,     /* a base pointer or stride is not 16-byte aligned            */
   KVC_E_TOO_LONG = -5,  /* a scored zone is longer than kvc_max_zone_len() (2^24), or a
-                           KVC_ALGO_STABLE selection zone longer than 16 384            */
+                           KVC_ALGO_STABLE selection zone longer than 65 536            */
   KVC_E_WORKSPACE = -6, /* workspace smaller than kvc_plan() reported                 */
   KVC_E_HIP = -7        /* a HIP launch failed                                        */
 };

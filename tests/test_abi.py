@@ -245,7 +245,7 @@ def test_attn_accumulate_validates_before_launching():
 
 def test_algo_enum_and_stable_zone_limit():
     """kvc_algo in the header equals the Python constants; kvc_plan accepts KVC_ALGO_STABLE for
-    zones up to 16 384 positions (KVC_E_TOO_LONG beyond, unless the indices are external) and
+    zones up to 65 536 positions (KVC_E_TOO_LONG beyond, unless the indices are external) and
     refuses unknown algorithms."""
     src = open(os.path.join(ROOT, "include", "kvc.h")).read()
     enum = re.search(r"enum kvc_algo \{([^}]*)\}", src).group(1)
@@ -254,7 +254,9 @@ def test_algo_enum_and_stable_zone_limit():
                     "KVC_ALGO_STABLE": N.KVC_ALGO_STABLE}
     ok = np.array([_layer(16384, 0, 16384, 512)], dtype=N.LAYER_DTYPE)
     assert N.plan(_params(algo=N.KVC_ALGO_STABLE), ok)[0] == 0
-    long = np.array([_layer(16448, 0, 16448, 512)], dtype=N.LAYER_DTYPE)
+    mid = np.array([_layer(65536, 0, 65536, 512)], dtype=N.LAYER_DTYPE)
+    assert N.plan(_params(algo=N.KVC_ALGO_STABLE), mid)[0] == 0
+    long = np.array([_layer(65600, 0, 65600, 512)], dtype=N.LAYER_DTYPE)
     assert N.plan(_params(algo=N.KVC_ALGO_STABLE), long.copy())[0] == N.KVC_E_TOO_LONG
     assert N.plan(_params(algo=N.KVC_ALGO_SORT), long.copy())[0] == 0
     assert N.plan(_params(algo=N.KVC_ALGO_STABLE, external_index=1,

@@ -6,8 +6,8 @@ CPU: the oracle's restatement (oracle.stable_prefix) against torch's own stable 
 bf16 / fp16 / fp32 rows with NaN / inf / signed zeros, both directions; the policy switch.
 GPU: the engine's radix selection through the C ABI against that oracle (every key variant, row
 lengths 17 .. 16 384, k at the edges, both launch shapes, snapkv scores), every method's golden
-inputs through the compress functions against the oracle's methods under the same policy, and
-zones past the LDS limit refused."""
+inputs through the compress functions against the oracle's methods under the same policy, zones
+past the LDS limit from the global-scratch kernel, and zones past 65 536 positions refused."""
 import numpy as np
 import pytest
 import torch
@@ -130,14 +130,35 @@ def test_methods_stable_policy_match_oracle(cid, launch, stable, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_stable_policy_refuses_zones_past_the_lds_limit(stable):
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("variant", ["normal", "few", "equal", "special"])
+@pytest.mark.parametrize("S", [16448, 40000, 65536])
+def test_abi_stable_select_global_scratch(dtype, variant, S):
+    """Zones past the LDS limit: the stable selection from the global-scratch kernel."""
+    from kvcompress import _native as N
+    from test_gpu_parity import _abi_select
+    K = prng.gen_keys(7500 + S, (1, 1, S, 32), dtype, variant)
+    for desc in (0, 1):
+        for k in (1, 512, S // 2, S - 1):
+            nrm, idx = _abi_select(K, k, desc, N.KVC_ALGO_STABLE)
+            ref = np.sort(oracle.stable_prefix(nrm, k, bool(desc)), axis=-1)
+            np.testing.assert_array_equal(idx, ref, err_msg=f"{dtype} {variant} S={S} k={k}")
+
+
+@pytest.mark.gpu
+def test_stable_policy_zone_limit(stable):
+    """Zones up to 65 536 positions select under the stable policy (matching the oracle); longer
+    ones raise."""
     from kvcompress.methods import fix_size_l2_compress
-    K = torch.randn(1, 2, 16400, 64, device="cuda:0").to(torch.bfloat16)
+    K = prng.gen_keys(7600, (1, 2, 20000, 64), "bf16", "normal")
+    V = prng.gen_values(7600, (1, 2, 20000, 64), "bf16")
+    out = fix_size_l2_compress([(to_dev(K), to_dev(V))], fix_kv_size=512, skip_layers=[])
+    rk, rv, _ = oracle.fix_size_l2_compress([(K, V)], fix_kv_size=512, skip_layers=[])[0]
+    np.testing.assert_array_equal(to_np(out[0][0]), rk)
+    np.testing.assert_array_equal(to_np(out[0][1]), rv)
+    L = torch.randn(1, 1, 65600, 32, device="cuda:0").to(torch.bfloat16)
     with pytest.raises(ValueError, match="stable tie policy"):
-        fix_size_l2_compress([(K, K)], fix_kv_size=512, skip_layers=[])
-    out = fix_size_l2_compress([(K[:, :, :16384], K[:, :, :16384])], fix_kv_size=512,
-                               skip_layers=[])
-    assert out[0][0].shape[2] == 512
+        fix_size_l2_compress([(L, L)], fix_kv_size=512, skip_layers=[])
 
 
 @pytest.mark.gpu
