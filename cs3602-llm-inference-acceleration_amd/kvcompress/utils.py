@@ -114,12 +114,21 @@ def key_length_attention(model, need_weights: bool = False):
               impl != KEY_LENGTH_EAGER and (need_weights or impl == "eager"))
     if switch:
         _register_eager()
-        model.set_attn_implementation(KEY_LENGTH_EAGER)
+        try:
+            model.set_attn_implementation(KEY_LENGTH_EAGER)
+        except (ValueError, TypeError, KeyError, NotImplementedError):
+            # a model class that refuses registered attention functions: its own eager kernel
+            # for the weights (ragged layer lengths then fail as they would without this)
+            if need_weights and impl != "eager":
+                model.set_attn_implementation("eager")
+            else:
+                switch = False
     try:
         yield
     finally:
         if switch:
             model.set_attn_implementation(impl)
+
 
 __all__ = ["to_dynamic_cache", "normalize_kv_cache", "get_cache_size_mb", "get_cache_info",
            "get_seq_len"]
