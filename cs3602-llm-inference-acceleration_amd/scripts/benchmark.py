@@ -305,9 +305,11 @@ _ARGS = (
     ("--random_model", str, None, "[offline] random-weight GPT-NeoX of this geometry"),
     ("--text_file", str, None, "[offline] samples from a local text file"),
     ("--synthetic_text", None, False, "[offline] deterministic pseudo-text samples"),
+    ("--tie_policy", str, "reference", "[extension] tie order of the selections: the "
+                                       "reference's (default) or stable (faster, not bit-exact)"),
 )
 _CHOICES = {"--method": _METHOD_CHOICES, "--pyramid_profile": ["exponential", "linear", "constant"],
-            "--random_model": sorted(RANDOM_MODELS)}
+            "--random_model": sorted(RANDOM_MODELS), "--tie_policy": ["reference", "stable"]}
 
 
 def build_parser():
@@ -327,6 +329,15 @@ def main(argv=None):
     args = parser.parse_args(argv)
     if not args.method and not args.compare_all and not args.compare_new:
         parser.error("Must specify --method, --compare_all, or --compare_new")
+    from kvcompress import _engine
+    prev = _engine.set_tie_policy(args.tie_policy)
+    try:
+        return _run(args)
+    finally:
+        _engine.set_tie_policy(prev)
+
+
+def _run(args):
     skip_layers = [int(x) for x in args.skip_layers.split(",")]
 
     print("=" * 70)
@@ -336,6 +347,8 @@ def main(argv=None):
     print(f"  Model: {args.random_model + ' (random weights)' if args.random_model else args.model_id}")
     print(f"  Method: {args.method or ('compare_all' if args.compare_all else 'compare_new')}")
     print(f"  Skip layers: {skip_layers}")
+    if args.tie_policy != "reference":
+        print(f"  Tie policy: {args.tie_policy} (not the reference's tie order)")
     print(f"  Number of samples: {args.num_samples}")
     print(f"  Max eval tokens: {args.max_tokens}")
     print(f"  Max new tokens: {args.max_new_tokens}")

@@ -89,3 +89,17 @@ def test_h2o_cli_compare_on_gpu(capsys):
     out = capsys.readouterr().out
     assert "h2o_attention_hh32" in out and "H2O-Attention:" in out
     assert "Test completed!" in out
+
+
+@pytest.mark.gpu
+def test_cli_stable_tie_policy_on_gpu(capsys):
+    """--tie_policy stable (extension): the run uses the stable selections and the previous
+    policy is restored afterwards."""
+    from kvcompress import _engine
+    mod = _cli()
+    res = _small_run(mod, ["--method", "fix_size_l2", "--fix_kv_sizes", "32", "--keep_ratios",
+                           "0.0", "--skip_layers", "0", "--tie_policy", "stable", "--no_baseline",
+                           "--no_recent_only"])
+    assert res and all(r["final_cache_size"] == 32 for r in res)
+    assert "Tie policy: stable" in capsys.readouterr().out
+    assert _engine.tie_policy == "reference"
