@@ -2,9 +2,12 @@
  * runtime API (no Python, no torch).  Test infrastructure (tests/test_native_abi.py).
  *
  *   abi_smoke plan                       host-only kvc_plan checks (no GPU needed)
- *   abi_smoke run DIR H S D K DESC       reads DIR/k.bin, DIR/v.bin (bf16 [1,H,S,D]), runs
+ *   abi_smoke run DIR H S D K DESC [ALGO]
+ *                                        reads DIR/k.bin, DIR/v.bin (bf16 [1,H,S,D]), runs
  *                                        fix_size_l2(keep K, keep_ratio 0) on one layer with
  *                                        kvc_plan + kvc_launch, writes DIR/k_out.bin, v_out.bin
+ *                                        (ALGO: kvc_algo, default KVC_ALGO_SORT; KVC_ALGO_STABLE
+ *                                        selects with the opt-in stable tie order)
  *
  * The mapping of one fix_size_l2 layer onto the C ABI is INTEGRATION.md's: zone [0, S),
  * n_select = K, no sink / tail, order ASC (keep_low) or DESC (keep_high), algo SORT
@@ -42,7 +45,7 @@ static kvc_layer_t layer_of(void* k, void* v, void* ko, void* vo, int H, int S, 
   return l;
 }
 
-static kvc_params_t params_of(int H, int D, int desc) {
+static kvc_params_t params_of(int H, int D, int desc, int algo) {
   kvc_params_t p;
   memset(&p, 0, sizeof(p));
   p.dtype = KVC_BF16;
@@ -50,7 +53,7 @@ static kvc_params_t params_of(int H, int D, int desc) {
   p.heads = H;
   p.head_dim = D;
   p.order = desc ? KVC_DESC : KVC_ASC;
-  p.algo = KVC_ALGO_SORT;
+  p.algo = algo;
   p.phases = KVC_PHASE_ALL;
   return p;
 }
@@ -62,17 +65,17 @@ static int plan_checks(void) {
   CHECK(kvc_source_digest() != NULL && strlen(kvc_source_digest()) > 0, "source digest");
   void* fake = (void*)(uintptr_t)4096; /* kvc_plan never dereferences tensor pointers */
   kvc_layer_t l = layer_of(fake, fake, fake, fake, 32, 16384, 128, 512);
-  kvc_params_t p = params_of(32, 128, 0);
+  kvc_params_t p = params_of(32, 128, 0, KVC_ALGO_SORT);
   kvc_plan_info_t info;
   CHECK(kvc_plan(&p, &l, 1, &info) == KVC_OK, "plan of the headline layer");
   CHECK(l.n_out == 512 && l.row0 == 0 && l.tile0 == 0, "plan-filled fields");
   CHECK(info.rows == 32 && info.workspace_bytes > 0, "plan info");
   p.head_dim = 100;
   CHECK(kvc_plan(&p, &l, 1, &info) == KVC_E_HEADDIM, "bad head_dim rejected");
-  p = params_of(32, 128, 0);
+  p = params_of(32, 128, 0, KVC_ALGO_SORT);
   p.dtype = 7;
   CHECK(kvc_plan(&p, &l, 1, &info) == KVC_E_DTYPE, "bad dtype rejected");
-  p = params_of(32, 128, 0);
+  p = params_of(32, 128, 0, KVC_ALGO_SORT);
   l.k = (void*)(uintptr_t)4098;
   CHECK(kvc_plan(&p, &l, 1, &info) == KVC_E_ALIGN, "misaligned pointer rejected");
   l.k = fake;
@@ -86,6 +89,11 @@ static int plan_checks(void) {
   p.reserved = 1;
   CHECK(kvc_plan(&p, &l, 1, &info) == KVC_E_ARG, "non-zero reserved field rejected");
   p.reserved = 0;
+  p.algo = KVC_ALGO_STABLE;
+  CHECK(kvc_plan(&p, &l, 1, &info) == KVC_OK, "stable selection planned");
+  p.algo = 3;
+  CHECK(kvc_plan(&p, &l, 1, &info) == KVC_E_ARG, "unknown algorithm rejected");
+  p.algo = KVC_ALGO_SORT;
   CHECK(strcmp(kvc_status_string(KVC_E_ALIGN), "pointer or stride not 16-byte aligned") == 0,
         "status string");
   printf("abi_smoke plan: ok\n");
@@ -113,7 +121,7 @@ static int write_file(const char* path, const void* buf, size_t bytes) {
   return put == bytes ? 0 : 1;
 }
 
-static int run(const char* dir, int H, int S, int D, int K, int desc) {
+static int run(const char* dir, int H, int S, int D, int K, int desc, int algo) {
   char path[4096];
   const size_t in_bytes = (size_t)H * S * D * 2, out_bytes = (size_t)H * K * D * 2;
   snprintf(path, sizeof(path), "%s/k.bin", dir);
@@ -129,7 +137,7 @@ static int run(const char* dir, int H, int S, int D, int K, int desc) {
             hipMemcpy(dv, hv, in_bytes, hipMemcpyHostToDevice) == hipSuccess,
         "upload");
   kvc_layer_t l = layer_of(dk, dv, dko, dvo, H, S, D, K);
-  kvc_params_t p = params_of(H, D, desc);
+  kvc_params_t p = params_of(H, D, desc, algo);
   kvc_plan_info_t info;
   CHECK(kvc_plan(&p, &l, 1, &info) == KVC_OK, "kvc_plan");
   CHECK(hipMalloc(&ws, info.workspace_bytes) == hipSuccess, "workspace");
@@ -159,9 +167,9 @@ static int run(const char* dir, int H, int S, int D, int K, int desc) {
 
 int main(int argc, char** argv) {
   if (argc >= 2 && strcmp(argv[1], "plan") == 0) return plan_checks();
-  if (argc == 8 && strcmp(argv[1], "run") == 0)
+  if ((argc == 8 || argc == 9) && strcmp(argv[1], "run") == 0)
     return run(argv[2], atoi(argv[3]), atoi(argv[4]), atoi(argv[5]), atoi(argv[6]),
-               atoi(argv[7]));
-  fprintf(stderr, "usage: abi_smoke plan | run DIR H S D K DESC\n");
+               atoi(argv[7]), argc == 9 ? atoi(argv[8]) : KVC_ALGO_SORT);
+  fprintf(stderr, "usage: abi_smoke plan | run DIR H S D K DESC [ALGO]\n");
   return 2;
 }

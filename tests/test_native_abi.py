@@ -30,14 +30,18 @@ def test_c_caller_plan_checks():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("algo", ["sort", "stable"])
 @pytest.mark.parametrize("desc", [0, 1])
-def test_c_caller_fix_size_l2_matches_oracle(tmp_path, desc):
+def test_c_caller_fix_size_l2_matches_oracle(tmp_path, desc, algo, monkeypatch):
     H, S, D, K = 4, 1000, 128, 100
     k = prng.gen_keys(321 + desc, (1, H, S, D), "bf16", "few")
     v = prng.gen_values(321 + desc, (1, H, S, D), "bf16")
     k.tofile(tmp_path / "k.bin")
     v.tofile(tmp_path / "v.bin")
-    r = subprocess.run([_exe(), "run", str(tmp_path), str(H), str(S), str(D), str(K), str(desc)],
+    if algo == "stable":  # KVC_ALGO_STABLE = 2; the oracle under the same policy
+        monkeypatch.setattr(oracle, "TIE", "stable")
+    r = subprocess.run([_exe(), "run", str(tmp_path), str(H), str(S), str(D), str(K), str(desc),
+                        "2" if algo == "stable" else "0"],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     ko = np.fromfile(tmp_path / "k_out.bin", dtype=np.uint16).reshape(1, H, K, D)
