@@ -180,3 +180,21 @@ def test_headline_geometry_stable_vs_reference_sets():
         eq = np.flatnonzero(v[0, h] == T)
         np.testing.assert_array_equal(np.sort(b[v[0, h][b] == T]), eq[:len(b[v[0, h][b] == T])])
     assert E.tie_policy == "reference"
+
+
+def test_tie_policy_from_environment():
+    """KVC_TIE_POLICY selects the policy at import; an unknown value refuses to import."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(root, "cs3602-llm-inference-acceleration_amd")
+    code = "import kvcompress._engine as E; print(E.tie_policy)"
+    env = dict(os.environ, PYTHONPATH=pkg, KVC_TIE_POLICY="stable")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and r.stdout.strip() == "stable", r.stderr
+    env["KVC_TIE_POLICY"] = "bogus"
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode != 0 and "KVC_TIE_POLICY" in r.stderr
