@@ -3,7 +3,9 @@ kvcompress/evaluate_attention.py) on a small random-weight GPT-NeoX.
 
 CPU: the harness runs end to end with the numpy oracle standing in for the manager and the
 compress call (test infrastructure), real attention weights reach the manager although the model
-is configured for sdpa, and the model's attention implementation is restored afterwards.
+is configured for sdpa, and the model's attention implementation is restored afterwards; the
+loops reproduce the UNMODIFIED reference's loops on the same CPU model exactly
+(tests/golden/eval_attention.json).
 GPU: the engine's manager + h2o_attention_compress against the oracle's -- identical caches at
 every step, so the PPL and accuracy match exactly (PPL delta 0), in fp32 / bf16 / fp16, and for a grouped-query Llama."""
 import numpy as np
@@ -140,3 +142,38 @@ def test_compare_h2o_methods_runs_on_engine():
     assert res[0]["final_cache_size"] == 559
     assert res[1]["final_cache_size"] == res[2]["final_cache_size"] == 512
     assert all(np.isfinite(r["perplexity"]) for r in res)
+
+
+def test_loops_reproduce_reference_golden(monkeypatch):
+    """The unmodified reference's loops on this CPU model (tests/golden/gen_eval_attention.py ->
+    eval_attention.json): the package's evaluate_with_compression (baseline, h2o_l2) and
+    evaluate_with_attention_compression (h2o_attention) over the oracle's compress / manager give
+    the reference's perplexity, accuracy and cache size exactly -- the same call sequence
+    (update, compress with its second accumulation, reset) on the same arithmetic."""
+    import json
+    import os
+    from kvcompress import evaluate_attention as EA
+    from kvcompress.evaluate import evaluate_with_compression
+    from test_ppl_parity import oracle_compress as oracle_method
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                       "eval_attention.json")))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(gold["threads"])
+    try:
+        model = toy_model(torch.float32, "cpu", layers=gold["layers"])
+        tok, text, kw, n = ToyTokenizer(512), TEXT * 2, gold["kw"], gold["max_tokens"]
+        got = {"baseline": evaluate_with_compression(model, tok, text, max_tokens=n,
+                                                     show_progress=False),
+               "h2o_l2": evaluate_with_compression(model, tok, text,
+                                                   compress_fn=oracle_method("h2o_l2"),
+                                                   compress_kwargs=kw, max_tokens=n,
+                                                   skip_layers=[0], show_progress=False)}
+        monkeypatch.setattr(EA, "h2o_attention_compress", oracle_compress)
+        got["h2o_attention"] = EA.evaluate_with_attention_compression(
+            model, tok, text, h2o_manager=OracleManager(**kw), max_tokens=n, skip_layers=[0],
+            show_progress=False, **kw)
+    finally:
+        torch.set_num_threads(prev)
+    for name, ref in gold["runs"].items():
+        for f in ("perplexity", "accuracy", "num_tokens", "final_cache_size"):
+            assert got[name][f] == ref[f], (name, f, got[name][f], ref[f])
