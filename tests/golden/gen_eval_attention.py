@@ -14,7 +14,9 @@ get a version that reads cache.layers[i].keys / .values; and transformers 5 retu
 weights only from eager attention, whose mask it no longer cuts to each layer's key length (the
 4.x eager kernels did), so the attention run uses the package's kvc_eager
 (kvcompress/utils.py key_length_attention, loaded by file path).  Writes data only
-(eval_attention.json): each run's perplexity, accuracy, token count and final cache size.
+(eval_attention.json): each run's perplexity, accuracy, token count and final cache size, and
+the same for every method configuration of tests/test_ppl_parity.py (CASES) through the
+reference's evaluate_with_compression.
 """
 import importlib.util
 import json
@@ -30,6 +32,7 @@ sys.path[:0] = [os.path.join(ROOT, "tests"), ROOT]
 THREADS = 8
 MAX_TOKENS = 700
 KW = dict(start_size=4, heavy_hitter_size=16, recent_size=40)
+FIELDS = ("perplexity", "accuracy", "num_tokens", "final_cache_size")
 
 
 def _v5_normalize(past_key_values):
@@ -74,12 +77,20 @@ def main():
                                                        max_tokens=MAX_TOKENS, skip_layers=[0],
                                                        show_progress=False, **KW)
     runs["h2o_attention"] = r
+    # every method of test_ppl_parity.CASES through the reference's own evaluate loop
+    from kvcompress.methods import get_compress_fn
+    from test_ppl_parity import CASES
+    methods = []
+    for name, kw in CASES:
+        r = R_eval.evaluate_with_compression(model, tok, text, compress_fn=get_compress_fn(name),
+                                             compress_kwargs=kw, max_tokens=MAX_TOKENS,
+                                             skip_layers=[0], show_progress=False)
+        methods.append({"name": name, "kwargs": kw, **{f: r[f] for f in FIELDS}})
     out = {"threads": THREADS, "max_tokens": MAX_TOKENS, "kw": KW, "layers": 3,
-           "text": "TEXT * 2", "runs": {k: {f: v[f] for f in ("perplexity", "accuracy",
-                                                             "num_tokens", "final_cache_size")}
-                                        for k, v in runs.items()}}
+           "text": "TEXT * 2", "runs": {k: {f: v[f] for f in FIELDS} for k, v in runs.items()},
+           "methods": methods}
     json.dump(out, open(os.path.join(HERE, "eval_attention.json"), "w"), indent=1)
-    print(json.dumps(out["runs"]))
+    print(json.dumps(out["runs"]), json.dumps(methods))
 
 
 if __name__ == "__main__":

@@ -177,3 +177,110 @@ def test_loops_reproduce_reference_golden(monkeypatch):
     for name, ref in gold["runs"].items():
         for f in ("perplexity", "accuracy", "num_tokens", "final_cache_size"):
             assert got[name][f] == ref[f], (name, f, got[name][f], ref[f])
+
+
+def _gold():
+    import json
+    import os
+    return json.load(open(os.path.join(os.path.dirname(__file__), "golden",
+                                       "eval_attention.json")))
+
+
+@pytest.mark.parametrize("i", range(len(_gold()["methods"])))
+def test_compression_loop_reproduces_reference_golden(i):
+    """Every method configuration of test_ppl_parity through the reference's own
+    evaluate_with_compression (eval_attention.json "methods") and through the package's, over
+    the oracle's compress: identical perplexity, accuracy, token count and cache size."""
+    from kvcompress.evaluate import evaluate_with_compression
+    from test_ppl_parity import oracle_compress as oracle_method
+    gold = _gold()
+    ref = gold["methods"][i]
+    prev = torch.get_num_threads()
+    torch.set_num_threads(gold["threads"])
+    try:
+        model = toy_model(torch.float32, "cpu", layers=gold["layers"])
+        got = evaluate_with_compression(model, ToyTokenizer(512), TEXT * 2,
+                                        compress_fn=oracle_method(ref["name"]),
+                                        compress_kwargs=ref["kwargs"],
+                                        max_tokens=gold["max_tokens"], skip_layers=[0],
+                                        show_progress=False)
+    finally:
+        torch.set_num_threads(prev)
+    for f in ("perplexity", "accuracy", "num_tokens", "final_cache_size"):
+        assert got[f] == ref[f], (ref["name"], ref["kwargs"], f, got[f], ref[f])
+
+
+def _to_gpu(t):
+    return None if t is None else t.to("cuda:0")
+
+
+def _engine_bridge(name):
+    """compress_fn for a CPU model: the layers go to the GPU, through the engine, and back."""
+    from kvcompress.methods import get_compress_fn
+    fn = get_compress_fn(name)
+
+    def run(kv_list, **kw):
+        out = fn([(_to_gpu(k), _to_gpu(v)) for k, v in kv_list], **kw)
+        return [(k.cpu(), v.cpu()) for k, v in out]
+    return run
+
+
+class _EngineManagerBridge:
+    """The engine's H2OAttentionManager (state on the GPU) behind a CPU model's loop."""
+
+    def __init__(self, **kw):
+        from kvcompress.methods.h2o_attention import H2OAttentionManager
+        self.inner = H2OAttentionManager(num_layers=3, num_heads=4, **kw)
+        self.inner.reduction_threads = THREADS
+
+    def reset(self):
+        self.inner.reset()
+
+    def update_attention_scores(self, attentions, skip_layers=()):
+        self.inner.update_attention_scores(
+            None if attentions is None else tuple(_to_gpu(a) for a in attentions), skip_layers)
+
+
+def _engine_h2o_attention_compress(kv_list, attention_scores=None, h2o_manager=None, **kw):
+    from kvcompress.methods.h2o_attention import h2o_attention_compress
+    out = h2o_attention_compress(
+        [(_to_gpu(k), _to_gpu(v)) for k, v in kv_list],
+        attention_scores=None if attention_scores is None else
+        tuple(_to_gpu(a) for a in attention_scores),
+        h2o_manager=h2o_manager.inner, **kw)
+    return [(k.cpu(), v.cpu()) for k, v in out]
+
+
+@pytest.mark.gpu
+def test_engine_reproduces_reference_loops_golden(monkeypatch):
+    """The reference's own runs (eval_attention.json) with the model on the CPU and every
+    compression on the HIP engine: every method's run and the attention-score run give the
+    reference's perplexity, accuracy and cache size exactly (PPL delta 0 against the unmodified
+    reference itself, not only against the oracle)."""
+    from kvcompress import _engine
+    from kvcompress import evaluate_attention as EA
+    from kvcompress.evaluate import evaluate_with_compression
+    gold = _gold()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(gold["threads"])
+    try:
+        model = toy_model(torch.float32, "cpu", layers=gold["layers"])
+        tok, text, n = ToyTokenizer(512), TEXT * 2, gold["max_tokens"]
+        for ref in gold["methods"]:
+            got = evaluate_with_compression(model, tok, text, compress_fn=_engine_bridge(ref["name"]),
+                                            compress_kwargs=ref["kwargs"], max_tokens=n,
+                                            skip_layers=[0], show_progress=False)
+            for f in ("perplexity", "accuracy", "num_tokens", "final_cache_size"):
+                assert got[f] == ref[f], (ref["name"], ref["kwargs"], f, got[f], ref[f])
+        monkeypatch.setattr(EA, "h2o_attention_compress", _engine_h2o_attention_compress)
+        kw = gold["kw"]
+        got = EA.evaluate_with_attention_compression(model, tok, text,
+                                                     h2o_manager=_EngineManagerBridge(**kw),
+                                                     max_tokens=n, skip_layers=[0],
+                                                     show_progress=False, **kw)
+        ref = gold["runs"]["h2o_attention"]
+        for f in ("perplexity", "accuracy", "num_tokens", "final_cache_size"):
+            assert got[f] == ref[f], ("h2o_attention", f, got[f], ref[f])
+    finally:
+        torch.set_num_threads(prev)
+    assert _engine.device_status(0) == 0
