@@ -16,7 +16,8 @@ weights only from eager attention, whose mask it no longer cuts to each layer's 
 (kvcompress/utils.py key_length_attention, loaded by file path).  Writes data only
 (eval_attention.json): each run's perplexity, accuracy, token count and final cache size, and
 the same for every method configuration of tests/test_ppl_parity.py (CASES) through the
-reference's evaluate_with_compression.
+reference's evaluate_with_compression, with the generating host's CPU model (the CPU forward's
+rounding is host-dependent: the tests that replay these runs skip on another CPU).
 """
 import importlib.util
 import json
@@ -33,6 +34,18 @@ THREADS = 8
 MAX_TOKENS = 700
 KW = dict(start_size=4, heavy_hitter_size=16, recent_size=40)
 FIELDS = ("perplexity", "accuracy", "num_tokens", "final_cache_size")
+
+
+def cpu_model():
+    """The host CPU's model name: the CPU model forward's rounding depends on the BLAS / oneDNN
+    kernels torch dispatches for it, so the runs are pinned to the host that made them."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def _v5_normalize(past_key_values):
@@ -87,6 +100,7 @@ def main():
                                              skip_layers=[0], show_progress=False)
         methods.append({"name": name, "kwargs": kw, **{f: r[f] for f in FIELDS}})
     out = {"threads": THREADS, "max_tokens": MAX_TOKENS, "kw": KW, "layers": 3,
+           "cpu_model": cpu_model(), "cpu_capability": torch.backends.cpu.get_cpu_capability(),
            "text": "TEXT * 2", "runs": {k: {f: v[f] for f in FIELDS} for k, v in runs.items()},
            "methods": methods}
     json.dump(out, open(os.path.join(HERE, "eval_attention.json"), "w"), indent=1)
