@@ -22,6 +22,10 @@
 #   heap       tools/heap_probe (register heap select vs std::partial_sort)      -> heap_probe.jsonl
 #   sq:LIB     SQ issue / wait counters of the headline SELECT_GATHER kernel with library LIB
 #              (kvcompress/_lib/LIB.so; two rocprofv3 --pmc passes of 8 SQ counters) -> sq_LIB.json
+#   tie        both tie policies (reference / stable, KVC_TIE_POLICY) on the bench workloads and
+#              the 8-way split's last rank                                     -> tie_ab.jsonl
+#   stamps:stable  s_memtime phases of the stable selection (diagnostic build
+#              tools/build_stamps.sh first; SEL_ALGO=2)                         -> stable_stamps.jsonl
 #   gatherprobe  tools/row_gather_probe (160-B row gathers, load shapes) timed, then FETCH_SIZE
 #              and the TCC read-request counters per shape (one rocprofv3 pass each)
 #                                                                                -> gprobe/
@@ -67,6 +71,30 @@ for step in "$@"; do
             >> "$O/workloads.jsonl" 2>> "$O/workloads.err" || { tail "$O/workloads.err"; exit 1; }
       done
       cat "$O/workloads.jsonl" ;;
+    tie)
+      : > "$O/tie_ab.jsonl"
+      for w in fix512-s16384 fix512-s4096 fix512-s4096-d80 h2o-s16384 snapkv-s16384 pyramid-s16384 adaptive-s16384; do
+        for pol in reference stable; do
+          KVC_TIE_POLICY=$pol timeout -k 10 300 python bench.py --workload $w --steps 20 --warmup 5 \
+              --no-cpu-baseline > "$O/tie_one.json" 2> "$O/tie_one.err" || { tail "$O/tie_one.err"; exit 1; }
+          python3 -c "import json; d=json.load(open('$O/tie_one.json')); print(json.dumps({'workload': '$w', 'policy': '$pol', 'ms_per_step': d['ms_per_step'], 'kernel_ms_per_step': d['kernel_ms_per_step']}))" >> "$O/tie_ab.jsonl"
+        done
+      done
+      for w in cfg4-h2o-l32 cfg5-snapkv-l32 cfg5-pyramid-l32; do
+        for pol in reference stable; do
+          KVC_TIE_POLICY=$pol timeout -k 10 200 python bench.py --workload $w --as-shard 7/8 --steps 50 \
+              --warmup 5 --no-cpu-baseline > "$O/tie_one.json" 2> "$O/tie_one.err" || { tail "$O/tie_one.err"; exit 1; }
+          python3 -c "import json; d=json.load(open('$O/tie_one.json')); print(json.dumps({'workload': '$w', 'shard': '7/8', 'policy': '$pol', 'ms_per_step': d['ms_per_step'], 'kernel_ms_per_step': d['kernel_ms_per_step']}))" >> "$O/tie_ab.jsonl"
+        done
+      done
+      cat "$O/tie_ab.jsonl" ;;
+    stamps:stable)
+      : > "$O/stable_stamps.jsonl"
+      for cfg in "" "SEL_L=4 SEL_S=15936 SEL_K=64" "SEL_S=4096"; do
+        env SEL_ALGO=2 $cfg timeout -k 10 120 python tools/select_stamps.py >> "$O/stable_stamps.jsonl" \
+            2> "$O/ss.err" || { tail "$O/ss.err"; exit 1; }
+      done
+      cat "$O/stable_stamps.jsonl" ;;
     shard)
       : > "$O/shard.jsonl"
       for w in cfg4-h2o-l32 cfg5-snapkv-l32 cfg5-pyramid-l32; do
