@@ -3245,11 +3245,10 @@ static int launch_select(const LayerChunk& T, int cn, int BH, int dt, int order,
     if (n_cap > kZoneMaxGlobal)  // u32 positions (the call's longest zone decides)
       return launch_k(select_long_kernel<KC>, rows_grid, dim3(kSelThreads), 0, s, T, BH, dt,
                       order, algo, norms, nstride, idx, istride, scratch, rb, n_cap, status);
-    if constexpr (!HH)
-      if (algo == KVC_ALGO_STABLE)
-        return launch_k(select_global_kernel<KC, true>, rows_grid, dim3(kSelThreads), 0, s, T, BH,
-                        dt, order, algo, norms, nstride, idx, istride, kWaveSeg, scratch, rb,
-                        n_cap, status);
+    if (algo == KVC_ALGO_STABLE)
+      return launch_k(select_global_kernel<KC, true>, rows_grid, dim3(kSelThreads), 0, s, T, BH,
+                      dt, order, algo, norms, nstride, idx, istride, kWaveSeg, scratch, rb, n_cap,
+                      status);
     return launch_k(select_global_kernel<KC>, rows_grid, dim3(kSelThreads), 0, s, T, BH, dt,
                     order, algo, norms, nstride, idx, istride, kWaveSeg, scratch, rb, n_cap,
                     status);
@@ -3267,8 +3266,7 @@ static int launch_select(const LayerChunk& T, int cn, int BH, int dt, int order,
                     BH, dt, order, algo, norms, nstride, idx, istride, kWaveSeg, n_cap, 0, stamps,
                     status);
   };
-  if constexpr (!HH)
-    if (algo == KVC_ALGO_STABLE) return go(std::true_type());
+  if (algo == KVC_ALGO_STABLE) return go(std::true_type());
   return go(std::false_type());
 }
 
@@ -3398,7 +3396,11 @@ static int attn_params_check(const kvc_attn_params_t* p, bool accumulate = false
   if (p->dtype != KVC_BF16 && p->dtype != KVC_F16 && p->dtype != KVC_F32) return KVC_E_DTYPE;
   if (p->batch < 1 || p->heads < 1) return KVC_E_ARG;
   // flags: kvc_attn_accumulate's KVC_ATTN_OLD_DTYPE(d) only (d a dtype other than p->dtype)
-  if (p->flags != 0 && (!accumulate || (p->flags & ~3) || p->flags == KVC_ATTN_OLD_DTYPE(p->dtype)))
+  // flags: KVC_ATTN_HH_STABLE (both entry points: one params struct serves a decode step's
+  // accumulate and heavy-hitter calls) | kvc_attn_accumulate's KVC_ATTN_OLD_DTYPE(d), bits 0-1,
+  // d a dtype other than p->dtype
+  const int od = p->flags & 3;
+  if ((p->flags & ~(3 | KVC_ATTN_HH_STABLE)) || (od && (!accumulate || od == KVC_ATTN_OLD_DTYPE(p->dtype))))
     return KVC_E_ARG;
   if (p->vec_bytes < 16 || p->vec_bytes > 64 || p->vec_bytes % 16) return KVC_E_ARG;
   if ((int64_t)p->batch * p->heads > 0x7FFFFFFF / kArgLayers) return KVC_E_ARG;
@@ -3411,13 +3413,14 @@ static int accumulate_impl(const kvc_attn_params_t* p, const kvc_attn_layer_t* l
   if (rc != KVC_OK) return rc;
   if (nl < 0 || (nl > 0 && !layers)) return KVC_E_ARG;
   const int es = esize(p->dtype);
-  const int odt = p->flags ? p->flags - 1 : p->dtype;  // acc_old's dtype
-  const int oes = esize(odt), nes = p->flags ? 4 : es;
+  const int od = p->flags & 3;                 // KVC_ATTN_OLD_DTYPE bits
+  const int odt = od ? od - 1 : p->dtype;      // acc_old's dtype
+  const int oes = esize(odt), nes = od ? 4 : es;
   for (int l = 0; l < nl; ++l) {
     const kvc_attn_layer_t& y = layers[l];
     if (!y.attn || !y.acc_new || y.q_len < 1 || y.key_len < 1 || y.old_len < 0 ||
         y.old_len > y.key_len || (y.old_len > 0 && !y.acc_old) || y.col_chunk < 0 ||
-        (p->flags && y.old_len == 0) || (uintptr_t)y.attn % es ||
+        (od && y.old_len == 0) || (uintptr_t)y.attn % es ||
         (uintptr_t)y.acc_new % nes || (uintptr_t)y.acc_old % oes)
       return KVC_E_ARG;
     if ((y.key_len + kColThreads * kAccCols - 1) / (kColThreads * kAccCols) > 65535)
@@ -3459,6 +3462,8 @@ static int hh_layout(const kvc_attn_params_t* p, const kvc_hh_layer_t* layers, i
         (uintptr_t)y.acc % esize(p->dtype))
       return KVC_E_ARG;
     if (y.zone_len > kZoneMaxLong) return KVC_E_TOO_LONG;
+    if ((p->flags & KVC_ATTN_HH_STABLE) && y.n_select < y.zone_len && y.zone_len > kZoneMaxGlobal)
+      return KVC_E_TOO_LONG;  // the stable selection's longest zone, as kvc_plan
     mmax = y.zone_len > mmax ? y.zone_len : mmax;
   }
   const int64_t rows = (int64_t)nl * p->batch;
@@ -3511,7 +3516,8 @@ static int heavy_hitters_impl(const kvc_attn_params_t* p, const kvc_hh_layer_t* 
                        vec_min, sums, nstride);
       if (r != KVC_OK) return r;
       // torch.topk(largest=True) + torch.sort: the descending TOPK selection, ascending indices
-      return launch_select<KC, true>(S, cn, B, DT, KVC_DESC, KVC_ALGO_TOPK, sums, nstride, o, ostride,
+      const int algo = (p->flags & KVC_ATTN_HH_STABLE) ? KVC_ALGO_STABLE : KVC_ALGO_TOPK;
+      return launch_select<KC, true>(S, cn, B, DT, KVC_DESC, algo, sums, nstride, o, ostride,
                                long_zone, scratch, nullptr, p->device_status, s);
     });
   }

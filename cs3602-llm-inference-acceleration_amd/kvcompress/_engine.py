@@ -162,8 +162,9 @@ split_select_gather = False
 # tied keys kept in position order -- the first k of argsort(stable=True), for argsort and topk
 # callers alike (KVC_ALGO_STABLE: a radix select, no partition chain).  The two differ only
 # where a tie straddles the k-th key, i.e. on most bf16 / fp16 rows.  KVC_TIE_POLICY=stable in
-# the environment selects it at import, set_tie_policy() at run time.  h2o_attention's
-# heavy hitters keep the reference order either way.
+# the environment selects it at import, set_tie_policy() at run time.  It covers h2o_attention's
+# heavy hitters too (KVC_ATTN_HH_STABLE: the first k of a stable descending sort of the head
+# sums).
 TIE_POLICIES = ("reference", "stable")
 STABLE_MAX_ZONE = 65536  # kvc.h KVC_ALGO_STABLE: the LDS and u16-position global kernels
 tie_policy = __import__("os").environ.get("KVC_TIE_POLICY", "reference")

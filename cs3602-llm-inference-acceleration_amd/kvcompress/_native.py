@@ -22,6 +22,9 @@ FLAG_SPLIT_SELECT_GATHER, FLAG_SHARED_INDEX, FLAG_GATHER_FIXED, FLAG_GATHER_SELE
 DEV_SELECT_BOUNDS, DEV_INDEX_RANGE = 1, 2  # enum kvc_device_status bits
 
 
+ATTN_HH_STABLE = 4  # kvc_attn_params.flags: kvc_heavy_hitters with the stable tie order
+
+
 def ATTN_OLD_DTYPE(d):
     """kvc_attn_params.flags of kvc_attn_accumulate: acc_old of dtype d (KVC_ATTN_OLD_DTYPE)."""
     return d + 1

@@ -35,6 +35,8 @@ def _attn_params(dtype, B, H, decay, device, old_dtype=None):
     then promotes to float32, h2o_attention.py:129-151; kvc_attn_accumulate's
     KVC_ATTN_OLD_DTYPE flag)."""
     flags = N.ATTN_OLD_DTYPE(_DT[old_dtype]) if old_dtype not in (None, dtype) else 0
+    if E.tie_policy == "stable":  # the heavy hitters' selection (kvc_heavy_hitters) only
+        flags |= N.ATTN_HH_STABLE
     return N.AttnParams(dtype=_DT[dtype], batch=B, heads=H, vec_bytes=CO.SUM_VEC_BYTES,
                         decay=float(np.float32(decay)), flags=flags,
                         device_status=E.status_word(device).data_ptr())
@@ -365,7 +367,7 @@ def _replay_step(kvl, attention_scores, mgr, start_size, heavy_hitter_size, rece
         key = (sig, start_size, heavy_hitter_size, recent_size, E._freeze(skip_layers),
                mgr.start_size, mgr.heavy_hitter_size, mgr.recent_size,
                float(np.float32(mgr.decay_factor)), mgr._threads(), E.split_select_gather,
-               torch.cuda.current_stream(sig[4]).cuda_stream)
+               E.tie_policy, torch.cuda.current_stream(sig[4]).cuda_stream)
     except TypeError:
         return None
     plan = step_memo.get(key)

@@ -210,15 +210,20 @@ typedef struct kvc_attn_params {
   int32_t vec_bytes;    /* SIMD width of the reference's CPU sum kernel: 32 on x86 (sum_stub has
                            no AVX512 variant) */
   float decay;          /* decay_factor as the fp32 value torch multiplies by (:136, :146) */
-  int32_t flags;        /* kvc_heavy_hitters: 0.  kvc_attn_accumulate: 0, or
+  int32_t flags;        /* kvc_heavy_hitters: 0 or KVC_ATTN_HH_STABLE.  kvc_attn_accumulate: 0, or
                            KVC_ATTN_OLD_DTYPE(d) when every layer's acc_old (old_len > 0 in every
                            layer) is of enum kvc_dtype d != dtype -- the reference then promotes
                            through `acc * decay`, torch.cat and `+` (:129-151): base is rounded to
-                           d, and acc_new is FLOAT32 = fp32(base) + fp32(attn.sum), unrounded */
+                           d, and acc_new is FLOAT32 = fp32(base) + fp32(attn.sum), unrounded --
+                           and/or KVC_ATTN_HH_STABLE, which it ignores (one struct per step) */
   uint32_t* device_status; /* optional, as kvc_params_t */
 } kvc_attn_params_t;
 
 #define KVC_ATTN_OLD_DTYPE(d) ((int32_t)(d) + 1) /* kvc_attn_params.flags, bits 0-1 */
+/* kvc_attn_params.flags bit 2 (opt-in): kvc_heavy_hitters selects the first n_select of a STABLE
+ * descending sort of the head sums (KVC_ALGO_STABLE's tie order) instead of torch.topk's; zones
+ * of at most 65 536 positions (else KVC_E_TOO_LONG). */
+#define KVC_ATTN_HH_STABLE 4
 
 /* One layer of update_attention_scores (:100-154). */
 typedef struct kvc_attn_layer {

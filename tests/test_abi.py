@@ -262,3 +262,21 @@ def test_algo_enum_and_stable_zone_limit():
     assert N.plan(_params(algo=N.KVC_ALGO_STABLE, external_index=1,
                           phases=N.PHASE_GATHER), long.copy())[0] == 0
     assert N.plan(_params(algo=3), ok.copy())[0] == -1  # KVC_E_ARG
+
+
+def test_heavy_hitter_stable_flag():
+    """KVC_ATTN_HH_STABLE: accepted by kvc_hh_workspace (zones up to 65 536 positions), unknown
+    flag bits refused."""
+    def p(flags):
+        return N.AttnParams(dtype=N.KVC_BF16, batch=1, heads=4, vec_bytes=32, decay=0.9,
+                            flags=flags, device_status=None)
+
+    def table(m):
+        t = np.zeros(1, dtype=N.HH_LAYER_DTYPE)
+        t[0] = (4096, m + 448, 4, m, 64, 0, 0)
+        return t
+    assert N.hh_workspace(p(N.ATTN_HH_STABLE), table(15936))[0] == 0
+    assert N.hh_workspace(p(0), table(70000))[0] == 0
+    assert N.hh_workspace(p(N.ATTN_HH_STABLE), table(70000))[0] == N.KVC_E_TOO_LONG
+    assert N.hh_workspace(p(8), table(15936))[0] == -1  # KVC_E_ARG
+    assert N.hh_workspace(p(N.ATTN_OLD_DTYPE(N.KVC_F32)), table(15936))[0] == -1  # accumulate only

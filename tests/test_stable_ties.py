@@ -198,3 +198,40 @@ def test_tie_policy_from_environment():
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                        timeout=300)
     assert r.returncode != 0 and "KVC_TIE_POLICY" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", ["bf16", "fp32"])
+@pytest.mark.parametrize("S", [3000, 16384])
+def test_h2o_attention_stable_heavy_hitters_match_oracle(dt, S, stable):
+    """h2o_attention under the stable policy: accumulations, heavy hitters (the first k of a
+    stable descending sort of the head sums: KVC_ATTN_HH_STABLE) and compressed K / V equal the
+    oracle manager's under the same policy, over three decode-shaped steps (tie-heavy
+    attention; the third step replayed natively)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import h2o_inputs
+    from oracle import h2o_oracle as HO
+    from kvcompress.methods import h2o_attention as HA
+    H, D, L = 4, 64, 2
+    kw = dict(start_size=4, heavy_hitter_size=64, recent_size=444)
+    kv = [(prng.gen_keys(8100 + li, (1, H, S, D), dt), prng.gen_values(8100 + li, (1, H, S, D), dt))
+          for li in range(L)]
+    kvd = [(to_dev(k), to_dev(v)) for k, v in kv]
+    mgr = HA.H2OAttentionManager(num_layers=L, num_heads=H, **kw)
+    mgr.reduction_threads = 8
+    omgr = HO.H2OManager(threads=8, **kw)
+    HA.step_memo.clear()
+    for st in range(3):
+        atts = [h2o_inputs.attention(9100 + 10 * st + li, H, 1, S, dt) for li in range(L)]
+        out = HA.h2o_attention_compress(list(kvd), attention_scores=tuple(to_dev(a) for a in atts),
+                                        h2o_manager=mgr, skip_layers=[], **kw)
+        ref = HO.h2o_attention_compress(kv, atts, omgr, skip_layers=[], **kw)
+        for li in range(L):
+            np.testing.assert_array_equal(to_np(mgr.accumulated_attention[li]), omgr.acc[li])
+            np.testing.assert_array_equal(mgr.get_heavy_hitter_indices(li, S).cpu().numpy(),
+                                          omgr.get_heavy_hitter_indices(li, S))
+            np.testing.assert_array_equal(to_np(out[li][0]), ref[li][0], err_msg=f"K {st} {li}")
+            np.testing.assert_array_equal(to_np(out[li][1]), ref[li][1], err_msg=f"V {st} {li}")
+    assert HA.step_stats["replayed"] >= 1
