@@ -3216,7 +3216,12 @@ static int launch_score(const LayerChunk& T, int nl, int H, int64_t tile_base,
 // `work` = max n_out over the chunk's layers; grid = (rows, token blocks)
 // KVC_FLAG_GATHER_FIXED launches (copies meant to run beside a selection on another stream) use
 // at most this many workgroups: two of four waves per CU
-constexpr int kFixedGatherBlocks = 512;
+// (A/B: an uncapped grid starves the heap select beside it -- the S = 16 384 h2o_attention call
+// 0.155 -> 0.216 ms, 1 024 blocks 0.208; tools/ab_variants.txt fgfull / fg1024)
+#ifndef KVC_FIXED_GATHER_BLOCKS
+#define KVC_FIXED_GATHER_BLOCKS 512
+#endif
+constexpr int kFixedGatherBlocks = KVC_FIXED_GATHER_BLOCKS;
 template <int DT, int NC>
 static int launch_gather(const LayerChunk& T, int nl, int H, int BH, const int32_t* idx,
                          int64_t istride, int shared, uint32_t* status, int64_t work, int part,
