@@ -28,7 +28,6 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
-sys.path[:0] = [os.path.join(ROOT, "tests"), ROOT]
 
 THREADS = 8
 MAX_TOKENS = 700
@@ -56,6 +55,7 @@ def _v5_normalize(past_key_values):
 
 
 def main():
+    sys.path[:0] = [os.path.join(ROOT, "tests"), ROOT]
     torch.set_num_threads(THREADS)
     import kvcompress  # the reference (PYTHONPATH=/root/reference)
     assert os.path.realpath(kvcompress.__file__).startswith("/root/reference"), kvcompress.__file__
