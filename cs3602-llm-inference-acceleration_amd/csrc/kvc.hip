@@ -1224,7 +1224,8 @@ __device__ __forceinline__ void p2_window0(const KeyT* key, uint16_t* spos, uint
 // Returns with the segment's final arrangement in key / idx (only the first-k SET matters).
 template <typename KeyT>
 __device__ __forceinline__ void wave_tiny_chain(KeyT* key, uint16_t* idx, int k, bool topk,
-                                                int thr, int lo, int hi, int depth) {
+                                                int thr, int lo, int hi, int depth,
+                                                uint32_t* status) {
   const int lane = threadIdx.x & 63;
   const int m = hi - lo;  // <= 64
   const bool own = lane < m;
@@ -1282,6 +1283,10 @@ __device__ __forceinline__ void wave_tiny_chain(KeyT* key, uint16_t* idx, int k,
     const bool sg = ge && A + lin < tot_le;        // g_t (t = A + 1) with g_t < s_t: swapped
     const uint64_t SG = __builtin_amdgcn_ballot_w64(sg);
     const int msw = __popcll(SG);
+    // the rank -> lane tables below use lane 63 as the sink of lanes with nothing to record:
+    // sound because the swapped pairs are disjoint in (slo, shi), so msw <= 31 ranks (lanes
+    // 0..30).  Checked (one scalar compare per level), never expected to fire.
+    if (msw > 31 && status && lane == 0) atomicOr(status, (uint32_t)KVC_DEV_INTERNAL);
     const int srk = tot_le - lin + 1;              // s rank of an le lane
     const bool ss = le && srk <= msw;              // s_t, t <= m: swapped
     // rank -> lane tables: lane t - 1 of gt / st receives g_t / s_t (others write lane 63,
@@ -1602,13 +1607,13 @@ template <typename KeyT, int NT, int MAXJ>
 __device__ __forceinline__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, uint16_t* gpos,
                          SelScalars<KeyT>& sc, int k, bool topk, int thr, int cap, int& lo,
                          int& hi, int& depth, int& level, int wave_seg,
-                         uint64_t* acc = nullptr) {
+                         uint64_t* acc = nullptr, uint32_t* status = nullptr) {
   const int tid = (NT == 64) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   while (true) {
     if (lo == k || hi == k) return 0;  // a partition boundary sits at k: the set is final
     if constexpr (NT == 64 && kTinyChain) {
       if (hi - lo <= 64 && hi - lo > thr) {  // the last levels from registers
-        wave_tiny_chain(key, idx, k, topk, thr, lo, hi, depth);
+        wave_tiny_chain(key, idx, k, topk, thr, lo, hi, depth, status);
         return 0;
       }
     }
@@ -2219,7 +2224,7 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
     KVC_STAMP(2);
     if (st == 1 && wid == 0)
       run_chain<KeyT, 64, 16>(key, idx, spos, A.gpos, sc, k, topk, thr, cap, lo, hi, depth,
-                              level, wave_seg, accw);
+                              level, wave_seg, accw, status);
   }
   __syncthreads();
   KVC_STAMP(3);
@@ -2767,8 +2772,14 @@ __global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT))
   const int r = wg % BH;
   if (ly->n_out == 0) return;
   const bool selects = layer_selects(*ly);
+  if constexpr (NT == kSelThreads) {
+    n_cap = kZoneMax;
+    cap = kSelCapBig<KeyT>;
+  }
   if (copier) {
-    if (selects)
+    // a row over the selecting workgroup's capacity is flagged there and left wholly unwritten
+    // (KVC_DEV_SELECT_BOUNDS): its sink / tail rows are not copied either
+    if (selects && ly->zone_len <= MAXN && ly->zone_len <= n_cap)
       with_dt<KC>(dt, [&](auto D) {
         gather_row<D.value, NC, NT, kSgNts>(ly, r, H, nullptr, PART_FIXED);
       });
@@ -2779,8 +2790,6 @@ __global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT))
   if constexpr (NT == kSelThreads) {
     __shared__ __attribute__((aligned(16))) char smem[kSelBytesBig<KeyT>];
     arrays = smem;
-    n_cap = kZoneMax;
-    cap = kSelCapBig<KeyT>;
   } else {
     extern __shared__ __attribute__((aligned(16))) char dsmem[];
     arrays = dsmem;
@@ -2793,7 +2802,8 @@ __global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT))
                                                                   nullptr, sel,
                                                     arrays, n_cap, cap, sc, wave_seg, nullptr,
                                                     status);
-    if (!ok) return;  // flagged in *status; the row's output is left unwritten
+    if (!ok) return;  // flagged in *status; the row's output is left unwritten (the copier
+                      // workgroup of a split row skips it too)
     __syncthreads();
   }
   with_dt<KC>(dt, [&](auto D) {

@@ -381,6 +381,9 @@ def status_word(device):
     w = _status_words.get(device)
     if w is None:
         w = _status_words[device] = _new_status_word(device)
+    t = getattr(_check_state, "touched", None)
+    if t is not None:  # inside a status-checked call: this device is read at its end
+        t.add(device)
     return w
 
 
@@ -415,7 +418,16 @@ check_status = _os.environ.get("KVC_CHECK_STATUS", "") not in ("", "0")
 _STATUS_BITS = ((N.DEV_SELECT_BOUNDS, "KVC_DEV_SELECT_BOUNDS (a selection row exceeded its "
                  "kernel's zone capacity: that row's output was left unwritten)"),
                 (N.DEV_INDEX_RANGE, "KVC_DEV_INDEX_RANGE (a caller-provided index lay outside its "
-                 "zone and was clamped)"))
+                 "zone and was clamped)"),
+                (N.DEV_INTERNAL, "KVC_DEV_INTERNAL (an internal invariant of the selection "
+                 "failed: that row's output is unspecified)"))
+
+# Per-thread state of the status check: `depth` counts the status-checked calls in progress
+# (h2o_attention_compress calls the manager's checked methods: only the outermost call reads
+# the words), `touched` collects the devices the outermost call's launches used.
+import threading as _threading
+
+_check_state = _threading.local()
 
 
 def set_status_check(on: bool = True):
@@ -425,9 +437,12 @@ def set_status_check(on: bool = True):
     return prev
 
 
-def raise_on_status():
-    """Read (and clear) every used device's status word; RuntimeError if any bit is set."""
-    for device in list(_status_words):
+def raise_on_status(devices=None):
+    """Read (and clear) the status words of `devices` (default: every device the engine has
+    used); RuntimeError if any bit is set."""
+    for device in list(_status_words) if devices is None else sorted(devices):
+        if device not in _status_words:
+            continue
         v = device_status(device, clear=True)
         if v:
             names = [txt for bit, txt in _STATUS_BITS if v & bit] or [f"unknown bits {v:#x}"]
@@ -435,16 +450,44 @@ def raise_on_status():
                                f"device status {v:#x}: " + "; ".join(names))
 
 
+def _checked_call(call, result_devices=None):
+    """Run call() as a status-checked entry point: with check_status on, the OUTERMOST such call
+    ends by reading the words of the devices its launches touched (status_word() calls during
+    the call, plus `result_devices(out)` for launches that bypass it -- the native replay).
+    No read while a CUDA graph is being captured (the read synchronises)."""
+    st = _check_state
+    if not check_status or getattr(st, "depth", 0) > 0:
+        return call()
+    st.depth, st.touched = 1, set()
+    try:
+        out = call()
+        touched = st.touched
+    finally:
+        st.depth, st.touched = 0, None
+    if result_devices is not None:
+        touched |= result_devices(out)
+    if touched and not torch.cuda.is_current_stream_capturing():
+        raise_on_status(touched)
+    return out
+
+
+def _output_devices(out):
+    """CUDA devices of the tensors of a compress result (a list of (K, V) pairs)."""
+    devs = set()
+    for kv in out if isinstance(out, (list, tuple)) else ():
+        for t in kv if isinstance(kv, (list, tuple)) else ():
+            if isinstance(t, torch.Tensor) and t.is_cuda:
+                devs.add(t.get_device())
+    return devs
+
+
 def status_checked(fn):
-    """Wrap an entry point so that, with check_status on, its calls end with raise_on_status()."""
+    """Wrap an entry point so that, with check_status on, its calls end with a status read."""
     import functools
 
     @functools.wraps(fn)
     def wrapper(*args, **kwargs):
-        out = fn(*args, **kwargs)
-        if check_status:
-            raise_on_status()
-        return out
+        return _checked_call(lambda: fn(*args, **kwargs))
     return wrapper
 
 
@@ -742,10 +785,8 @@ def memoized(fn):
 
     @functools.wraps(fn)
     def wrapper(past_key_values, *args, **kwargs):
-        out = _memo_call(past_key_values, *args, **kwargs)
-        if check_status:
-            raise_on_status()
-        return out
+        return _checked_call(lambda: _memo_call(past_key_values, *args, **kwargs),
+                             _output_devices)
 
     def _memo_call(past_key_values, *args, **kwargs):
         global _recording

@@ -19,7 +19,7 @@ KVC_ALGO_SORT, KVC_ALGO_TOPK, KVC_ALGO_STABLE = 0, 1, 2
 KVC_SCORE_NORM, KVC_SCORE_SNAPKV = 0, 1
 PHASE_SCORE, PHASE_SELECT, PHASE_GATHER, PHASE_ALL = 1, 2, 4, 7
 FLAG_SPLIT_SELECT_GATHER, FLAG_SHARED_INDEX, FLAG_GATHER_FIXED, FLAG_GATHER_SELECTED = 1, 2, 4, 8
-DEV_SELECT_BOUNDS, DEV_INDEX_RANGE = 1, 2  # enum kvc_device_status bits
+DEV_SELECT_BOUNDS, DEV_INDEX_RANGE, DEV_INTERNAL = 1, 2, 4  # enum kvc_device_status bits
 
 
 ATTN_HH_STABLE = 4  # kvc_attn_params.flags: kvc_heavy_hitters with the stable tie order
@@ -29,7 +29,7 @@ def ATTN_OLD_DTYPE(d):
     """kvc_attn_params.flags of kvc_attn_accumulate: acc_old of dtype d (KVC_ATTN_OLD_DTYPE)."""
     return d + 1
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 KVC_E_TOO_LONG = -5
 
 # struct kvc_layer (include/kvc.h) -- 136 bytes, checked against kvc_layer_struct_size()

@@ -47,7 +47,12 @@
 extern "C" {
 #endif
 
-#define KVC_ABI_VERSION 3
+/* ABI history:
+ *   3  kvc_params_t.flags / reserved / device_status; the h2o_attention entries.
+ *   4  KVC_ALGO_STABLE and KVC_ATTN_HH_STABLE (opt-in stable tie policy); KVC_FLAG_GATHER_FIXED /
+ *      KVC_FLAG_GATHER_SELECTED are refused (KVC_E_ARG) without external_index, where a v3
+ *      library accepted them; device status bit KVC_DEV_INTERNAL. */
+#define KVC_ABI_VERSION 4
 
 typedef struct ihipStream_t* kvc_stream_t; /* a hipStream_t; NULL = legacy default stream */
 
@@ -89,10 +94,15 @@ enum kvc_flag {
 /* Bits the kernels OR into *params.device_status (when not NULL).  The word is sticky: the
  * library never clears it; the caller zeroes it and reads it after the stream has drained. */
 enum kvc_device_status {
-  KVC_DEV_SELECT_BOUNDS = 1, /* a selection row exceeded its kernel's zone capacity: that row's
-                                output is unspecified (never expected: kvc_launch picks kernels
-                                by the planned zone lengths)                                  */
-  KVC_DEV_INDEX_RANGE = 2    /* an external index lay outside its zone and was clamped        */
+  KVC_DEV_SELECT_BOUNDS = 1, /* a selection row exceeded its kernel's zone capacity: nothing
+                                is selected and none of that row's output rows is written
+                                (never expected: kvc_launch picks kernels by the planned zone
+                                lengths)                                                       */
+  KVC_DEV_INDEX_RANGE = 2,   /* an external index lay outside its zone and was clamped        */
+  KVC_DEV_INTERNAL = 4       /* an internal invariant of a selection failed (e.g. the register
+                                tail of the partition chain saw more swaps than a 64-lane
+                                segment allows): that row's output is unspecified (never
+                                expected; checked so a violation cannot pass silently)        */
 };
 enum kvc_status {
   KVC_OK = 0,

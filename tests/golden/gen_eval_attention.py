@@ -17,7 +17,12 @@ weights only from eager attention, whose mask it no longer cuts to each layer's 
 (eval_attention.json): each run's perplexity, accuracy, token count and final cache size, and
 the same for every method configuration of tests/test_ppl_parity.py (CASES) through the
 reference's evaluate_with_compression, with the generating host's CPU model (the CPU forward's
-rounding is host-dependent: the tests that replay these runs skip on another CPU).
+rounding is host-dependent: the tests that replay these runs skip on another CPU).  Since round
+6 every compress call of the h2o_l2 run and of the method runs is also recorded step by step
+(tests/golden/step_digest.py: a digest of the call's input keys and of the positions it kept,
+recovered from position-encoding values), so that another host can check the engine's
+selections against the reference's at every step where its forward reproduces the keys, and
+name the first step where it does not.
 """
 import importlib.util
 import json
@@ -55,7 +60,8 @@ def _v5_normalize(past_key_values):
 
 
 def main():
-    sys.path[:0] = [os.path.join(ROOT, "tests"), ROOT]
+    sys.path[:0] = [os.path.join(ROOT, "tests"), ROOT, HERE]
+    from step_digest import Recorder
     torch.set_num_threads(THREADS)
     import kvcompress  # the reference (PYTHONPATH=/root/reference)
     assert os.path.realpath(kvcompress.__file__).startswith("/root/reference"), kvcompress.__file__
@@ -80,10 +86,12 @@ def main():
     r = R_eval.evaluate_with_compression(model, tok, text, compress_fn=None,
                                          max_tokens=MAX_TOKENS, show_progress=False)
     runs["baseline"] = r
-    r = R_eval.evaluate_with_compression(model, tok, text, compress_fn=h2o_l2_compress,
+    rec = Recorder(h2o_l2_compress)
+    r = R_eval.evaluate_with_compression(model, tok, text, compress_fn=rec,
                                          compress_kwargs=KW, max_tokens=MAX_TOKENS,
                                          skip_layers=[0], show_progress=False)
     runs["h2o_l2"] = r
+    steps = {"h2o_l2": rec.packed()}
     mgr = H2OAttentionManager(num_layers=3, num_heads=4, **KW)
     with ours.key_length_attention(model, need_weights=True):
         r = R_attn.evaluate_with_attention_compression(model, tok, text, h2o_manager=mgr,
@@ -95,16 +103,18 @@ def main():
     from test_ppl_parity import CASES
     methods = []
     for name, kw in CASES:
-        r = R_eval.evaluate_with_compression(model, tok, text, compress_fn=get_compress_fn(name),
+        rec = Recorder(get_compress_fn(name))
+        r = R_eval.evaluate_with_compression(model, tok, text, compress_fn=rec,
                                              compress_kwargs=kw, max_tokens=MAX_TOKENS,
                                              skip_layers=[0], show_progress=False)
-        methods.append({"name": name, "kwargs": kw, **{f: r[f] for f in FIELDS}})
+        methods.append({"name": name, "kwargs": kw, **{f: r[f] for f in FIELDS},
+                        "steps": rec.packed()})
     out = {"threads": THREADS, "max_tokens": MAX_TOKENS, "kw": KW, "layers": 3,
            "cpu_model": cpu_model(), "cpu_capability": torch.backends.cpu.get_cpu_capability(),
            "text": "TEXT * 2", "runs": {k: {f: v[f] for f in FIELDS} for k, v in runs.items()},
-           "methods": methods}
+           "methods": methods, "steps": steps}
     json.dump(out, open(os.path.join(HERE, "eval_attention.json"), "w"), indent=1)
-    print(json.dumps(out["runs"]), json.dumps(methods))
+    print(json.dumps(out["runs"]), json.dumps([{f: m[f] for f in FIELDS} for m in methods]))
 
 
 if __name__ == "__main__":

@@ -265,6 +265,20 @@ def build_cases():
         [L((1, 2, 30, 64), s + 358)], "recent0_quirk")
     add("evict_for_space", {"num_coming": 100, "start_size": 0, "recent_size": 1020}, "bf16",
         [L((1, 32, 16384, 80), s + 359)], "S16384_D80")
+    # ---- round 6: fp32 -- the dtype of the reference's own published runs (scripts/benchmark.py
+    # loads the model with no torch_dtype) -- at the BASELINE geometries: the untied radix fast
+    # path (headline), fp32 snapkv scoring + introselect (cfg5), h2o_l2's middle (cfg4), and a
+    # tie-heavy headline row set that takes the partition chain at 16 384 positions ----
+    add("fix_size_l2", {"fix_kv_size": 512, "keep_ratio": 0.0, "strategy": "keep_low",
+                        "skip_layers": []}, "fp32", [L((1, 32, 16384, 128), s + 400)],
+        "headline_fp32")
+    add("snapkv_lite", {"observation_window": 32, "keep_size": 512, "pooling_kernel": 5}, "fp32",
+        [L((1, 32, 16384, 128), s + 401)], "cfg5_S16384_pk5_fp32")
+    add("h2o_l2", {"start_size": 4, "heavy_hitter_size": 64, "recent_size": 444}, "fp32",
+        [L((1, 32, 16384, 80), s + 402)], "cfg4_S16384_D80_fp32")
+    add("fix_size_l2", {"fix_kv_size": 512, "keep_ratio": 0.0, "strategy": "keep_low",
+                        "skip_layers": []}, "fp32", [L((1, 8, 16384, 128), s + 403, "few")],
+        "headline_fp32_ties")
 
 
 def method_fn(name):

@@ -40,7 +40,7 @@ def test_struct_layout():
     assert ctypes.sizeof(N.PlanInfo) == 64
     assert ctypes.sizeof(N.AttnParams) == 32
     assert N.ATTN_LAYER_DTYPE.itemsize == 64 and N.HH_LAYER_DTYPE.itemsize == 32
-    assert L.kvc_version() == N.ABI_VERSION == 3
+    assert L.kvc_version() == N.ABI_VERSION == 4
     assert L.kvc_max_zone_len() == 1 << 24
 
 

@@ -14,6 +14,7 @@ import torch
 
 from gpu_util import to_dev, to_np
 from oracle import h2o_oracle as HO
+from step_digest import Recorder, first_divergence, unpack
 from test_ppl_parity import TEXT, ToyTokenizer, gqa_model, toy_model
 
 KW = dict(start_size=4, heavy_hitter_size=16, recent_size=40)
@@ -173,10 +174,10 @@ def test_loops_reproduce_reference_golden(monkeypatch):
     try:
         model = toy_model(torch.float32, "cpu", layers=gold["layers"])
         tok, text, kw, n = ToyTokenizer(512), TEXT * 2, gold["kw"], gold["max_tokens"]
+        rec = Recorder(oracle_method("h2o_l2"))
         got = {"baseline": evaluate_with_compression(model, tok, text, max_tokens=n,
                                                      show_progress=False),
-               "h2o_l2": evaluate_with_compression(model, tok, text,
-                                                   compress_fn=oracle_method("h2o_l2"),
+               "h2o_l2": evaluate_with_compression(model, tok, text, compress_fn=rec,
                                                    compress_kwargs=kw, max_tokens=n,
                                                    skip_layers=[0], show_progress=False)}
         monkeypatch.setattr(EA, "h2o_attention_compress", oracle_compress)
@@ -188,6 +189,8 @@ def test_loops_reproduce_reference_golden(monkeypatch):
     for name, ref in gold["runs"].items():
         for f in ("perplexity", "accuracy", "num_tokens", "final_cache_size"):
             assert got[name][f] == ref[f], (name, f, got[name][f], ref[f])
+    # every compress call: the same input keys and the same kept positions as the reference's
+    assert rec.steps == unpack(gold["steps"]["h2o_l2"])
 
 
 def _gold():
@@ -211,15 +214,17 @@ def test_compression_loop_reproduces_reference_golden(i):
     torch.set_num_threads(gold["threads"])
     try:
         model = toy_model(torch.float32, "cpu", layers=gold["layers"])
+        rec = Recorder(oracle_method(ref["name"]))
         got = evaluate_with_compression(model, ToyTokenizer(512), TEXT * 2,
-                                        compress_fn=oracle_method(ref["name"]),
-                                        compress_kwargs=ref["kwargs"],
+                                        compress_fn=rec, compress_kwargs=ref["kwargs"],
                                         max_tokens=gold["max_tokens"], skip_layers=[0],
                                         show_progress=False)
     finally:
         torch.set_num_threads(prev)
     for f in ("perplexity", "accuracy", "num_tokens", "final_cache_size"):
         assert got[f] == ref[f], (ref["name"], ref["kwargs"], f, got[f], ref[f])
+    # every compress call: the same input keys and the same kept positions as the reference's
+    assert rec.steps == unpack(ref["steps"])
 
 
 def _to_gpu(t):
@@ -305,4 +310,56 @@ def test_engine_loops_with_cpu_model_match_oracle_loops(monkeypatch):
             assert a[f] == b[f], ("h2o_attention", f, a[f], b[f])
     finally:
         torch.set_num_threads(prev)
+    assert _engine.device_status(0) == 0
+
+
+@pytest.mark.gpu
+def test_engine_loop_selections_match_reference_steps():
+    """The reference's loops step by step, on this host (eval_attention.json "steps", recorded
+    by tests/golden/gen_eval_attention.py from the unmodified reference): the same loop with the
+    model on this host's CPU and every compress call on the HIP engine, each call recorded the
+    same way (tests/golden/step_digest.py).  At every step whose input keys equal the
+    reference's -- i.e. until this host's CPU forward first rounds differently -- the engine must
+    have kept exactly the reference's positions; a run whose keys never diverge must also give
+    the reference's perplexity.  The first diverging step of every method is reported
+    (KVC_LOOP_REPORT=path writes the report as JSON): there the engine's every earlier selection
+    equalled the reference's, so the caches were identical, and the keys differ because the new
+    token's forward did."""
+    import json
+    import os
+    from kvcompress import _engine
+    from kvcompress.evaluate import evaluate_with_compression
+    from gen_eval_attention import cpu_model
+    gold = _gold()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(gold["threads"])
+    fields = ("perplexity", "accuracy", "num_tokens", "final_cache_size")
+    runs = [("h2o_l2", gold["kw"], gold["steps"]["h2o_l2"], gold["runs"]["h2o_l2"])]
+    runs += [(m["name"], m["kwargs"], m["steps"], m) for m in gold["methods"]]
+    report = {"host_cpu": cpu_model(), "golden_cpu": gold["cpu_model"], "runs": []}
+    try:
+        model = toy_model(torch.float32, "cpu", layers=gold["layers"])
+        for name, kw, steps, ref in runs:
+            rec = Recorder(_engine_bridge(name))
+            got = evaluate_with_compression(model, ToyTokenizer(512), TEXT * 2, compress_fn=rec,
+                                            compress_kwargs=kw, max_tokens=gold["max_tokens"],
+                                            skip_layers=[0], show_progress=False)
+            want = unpack(steps)
+            n, div, bad = first_divergence(rec.steps, want)
+            report["runs"].append({"method": name, "kwargs": kw, "steps": len(want),
+                                   "steps_with_equal_keys": n, "first_key_divergence": div,
+                                   "selection_mismatches_before_it": bad,
+                                   "ppl": got["perplexity"], "ref_ppl": ref["perplexity"]})
+            assert not bad, (name, kw, "engine selections differ from the reference's", bad[:5])
+            assert len(rec.steps) == len(want)
+            if div is None:  # this host's forward reproduced every step's keys
+                for f in fields:
+                    assert got[f] == ref[f], (name, kw, f, got[f], ref[f])
+    finally:
+        torch.set_num_threads(prev)
+        path = os.environ.get("KVC_LOOP_REPORT")
+        if path:
+            with open(path, "w") as f:
+                json.dump(report, f, indent=1)
+        print(json.dumps(report))
     assert _engine.device_status(0) == 0
