@@ -82,6 +82,12 @@ constexpr bool kSgNts = KVC_SG_NTS;
 #define KVC_SG_NTL false
 #endif
 constexpr bool kSgNtl = KVC_SG_NTL;
+// SELECT_GATHER rows touch the rows they already know they keep while wave 0 finishes the chain
+// (select_body; diagnostic A/B, off)
+#ifndef KVC_SG_PREFETCH
+#define KVC_SG_PREFETCH 0
+#endif
+constexpr bool kSgPrefetch = KVC_SG_PREFETCH;
 // the wave chain's segments of <= 64 positions in registers (wave_tiny_chain); 0: LDS levels
 #ifndef KVC_TINY_CHAIN
 #define KVC_TINY_CHAIN 1
@@ -279,9 +285,15 @@ __host__ __device__ constexpr int score_waves(int nc) {
 // One 64-token tile of one (layer, b, h) row: coalesced 16-B loads -> per-wave LDS slab ->
 // one lane per token, torch.norm's 8-accumulator FMA order (fp16: its serial order).  `wl` is
 // this wave's slab (kTile * ROWB bytes).
+// snapkv_lite rows (KVC_SCORE_SNAPKV) also get each tile's maximum stored norm, as the bits of
+// the stored value (u16 for 16-bit dtypes, u32 for fp32) in tmax[row * tmax_stride + tile]: a
+// norm is never negative (nor -0: the accumulators start at +0 and add squares), so the bit
+// order is the value order and every NaN's bits exceed +inf's.  The select kernel forms the
+// row's `max(norms)` (snapkv_lite.py:99) from them without a block reduction.
 template <int DT, int NC, bool NTL = false>
 __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int tt, int H,
-                                           char* wl, char* norms, int64_t norm_stride) {
+                                           char* wl, char* norms, int64_t norm_stride,
+                                           uint32_t* tmax, int64_t tmax_stride) {
   constexpr int ESZ = DTypeTraits<DT>::esz;
   constexpr int CP = score_cp(NC);  // 16-B chunks per token per phase
   constexpr int NPH = NC / CP;
@@ -330,6 +342,7 @@ __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int t
     }
     wave_sync();
   }
+  uint32_t bits = 0;  // the stored norm's bits (0 for lanes past the zone)
   if (lane < ntok) {
     float s = acc[0];
 #pragma unroll
@@ -339,18 +352,25 @@ __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int t
     // non-temporal: the select phase reads the norms back from the Infinity Cache, not from
     // this XCD's L2, so keeping them in L2 only evicts key lines (2.5% faster score pass)
     if constexpr (DT != KVC_F32) {
-      __builtin_nontemporal_store((uint16_t)bits16_dt<DT>(r),
-                                  reinterpret_cast<uint16_t*>(nrow) + tok0 + lane);
+      bits = bits16_dt<DT>(r);
+      __builtin_nontemporal_store((uint16_t)bits, reinterpret_cast<uint16_t*>(nrow) + tok0 + lane);
     } else {
+      bits = f32_to_bits(r);
       __builtin_nontemporal_store(r, reinterpret_cast<float*>(nrow) + tok0 + lane);
     }
+  }
+  if (ly->score_mode == KVC_SCORE_SNAPKV && tmax) {  // wave-uniform
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) bits = max(bits, (uint32_t)__shfl_xor((int)bits, o, 64));
+    if (lane == 0) tmax[(int64_t)(ly->row0 + row) * tmax_stride + tt] = bits;
   }
 }
 
 template <int DT, int NC, bool NTL>
 __global__ void __launch_bounds__(score_waves(NC) * 64)
     score_kernel(const LayerChunk T, int nl, int H, int64_t tile_base, int64_t chunk_tiles,
-                 char* __restrict__ norms, int64_t norm_stride) {
+                 char* __restrict__ norms, int64_t norm_stride, uint32_t* __restrict__ tmax,
+                 int64_t tmax_stride) {
   constexpr int CP = score_cp(NC);
   constexpr int ROWB = score_rowb(CP);
   constexpr int kScoreWaves = score_waves(NC);
@@ -373,7 +393,8 @@ __global__ void __launch_bounds__(score_waves(NC) * 64)
     const int tpr = (ly->zone_len + kTile - 1) / kTile;
     const int local = (int)(g - ly->tile0);
     const int row = local / tpr;
-    score_tile<DT, NC, NTL>(ly, row, local - row * tpr, H, lds[wid], norms, norm_stride);
+    score_tile<DT, NC, NTL>(ly, row, local - row * tpr, H, lds[wid], norms, norm_stride, tmax,
+                            tmax_stride);
   }
 }
 
@@ -513,20 +534,156 @@ __device__ __forceinline__ float div5_rn(float x) {
   return (r == 0.0f || __builtin_isinf(q0)) ? q0 : __builtin_fmaf(r, 0.2f, q0);
 }
 
+// The pooled key vector of positions 8v .. 8v+7 (default pooling kernel 5, or none) from the
+// 16-bit scores of positions 8v-8 .. 8v+15 as floats in sw[0..24) (only 8v-2 .. 8v+9 are read;
+// terms outside [hs, he) are skipped): avg_pool1d's window sums in its order, / 5 by div5_rn,
+// rounded to the dtype, mapped to sort keys; positions past n get 0.
+template <int DT>
+__device__ __forceinline__ uint4 snapkv_pool_vec(const float (&sw)[24], int v, int n, bool pool,
+                                                 bool desc) {
+  uint32_t o[4] = {0, 0, 0, 0};
+  if constexpr (DT == KVC_BF16) {
+    // bf16: pairs of positions with packed fp32 adds, one hardware convert and one packed key
+    // map per pair (key_bf16x2 codes for every key of the row).  The window sums drop
+    // avg_pool1d's leading 0 + s: it only turns a -0 into +0, and the keys equate the two.
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const bool inner = pool && v >= 1 && v * 8 + 10 <= n;  // every window of the vector whole
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      f2 r;
+      if (inner) {
+        f2 acc = f2{sw[2 * p + 6], sw[2 * p + 7]};
+#pragma unroll
+        for (int t = 1; t < 5; ++t) acc = acc + f2{sw[2 * p + 6 + t], sw[2 * p + 7 + t]};
+        r = f2{div5_rn(acc.x), div5_rn(acc.y)};
+      } else {
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int e = 2 * p + b, i = v * 8 + e;
+          float x = sw[8 + e];
+          if (pool) {  // pool_k == 5, pad 2: window [i - 2, i + 3) clipped to [0, n), / 5
+            int hs = i - 2;
+            int he = min(hs + 5, n + 2);
+            const int psize = he - hs;
+            hs = max(hs, 0);
+            he = min(he, n);
+            float sum = 0.f;
+#pragma unroll
+            for (int t = 0; t < 5; ++t) {
+              const int j = i - 2 + t;
+              if (j >= hs && j < he) sum = sum + sw[8 + e - 2 + t];
+            }
+            x = psize == 5 ? div5_rn(sum) : sum / (float)psize;
+          }
+          r[b] = x;
+        }
+      }
+      const int i0 = v * 8 + 2 * p;
+      o[p] = key_bf16x2(f32x2_to_bf16x2_hw(r.x, r.y), desc) &
+             (i0 + 1 < n ? 0xFFFFFFFFu : i0 < n ? 0x0000FFFFu : 0u);
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int i = v * 8 + e;
+      float r;
+      if (pool) {  // pool_k == 5, pad 2: window [i - 2, i + 3) clipped to [0, n), / 5
+        int hs = i - 2;
+        int he = min(hs + 5, n + 2);
+        const int psize = he - hs;
+        hs = max(hs, 0);
+        he = min(he, n);
+        float sum = 0.f;
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+          const int j = i - 2 + t;
+          if (j >= hs && j < he) sum = sum + sw[8 + e - 2 + t];
+        }
+        r = psize == 5 ? div5_rn(sum) : sum / (float)psize;
+      } else {
+        r = sw[8 + e];
+      }
+      o[e >> 1] |= (i < n ? (uint32_t)key16_dt<DT>(out16<DT>(r), desc) : 0u) << (16 * (e & 1));
+    }
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// 16-bit scores s = dt(m - norm) of the two positions of a norm dword (the positions' order in
+// the dword kept): bf16 by one hardware convert per pair (NaN payloads unobserved), fp16 by the
+// hardware converts.
+template <int DT>
+__device__ __forceinline__ uint32_t snapkv_score_pair(float m, uint32_t w) {
+  if constexpr (DT == KVC_BF16)
+    return f32x2_to_bf16x2_hw(m - bf16_to_f32(w), m - bits_to_f32(w & 0xFFFF0000u));
+  else
+    return out16<DT>(m - in16<DT>(w & 0xFFFFu)) | (out16<DT>(m - in16<DT>(w >> 16)) << 16);
+}
+
 // snapkv_keys for 16-bit scores on LDS rows (n <= MAXV * 8 * NT): the same arithmetic per
-// position, with the row's norms read once as 16-B vectors (kept in registers for the max and
-// the scores), scores stored as 16-B vectors, and -- for the default pooling kernel 5 (and no
-// pooling) -- each thread pooling 8 consecutive positions from three 16-B reads of the scores
-// (the window sums add the same terms in the same order; terms outside [hs, he) are skipped).
-// Other pooling kernels pool one position at a time as snapkv_keys does.  `key`, `tmp` and
-// `nrow` are 16-B aligned; norm rows are padded to a multiple of 64 elements.
+// position (snapkv_lite.py:96-121), each thread making the keys of 8 consecutive positions.
+// `key`, `idx`, `tmp` and `nrow` are 16-B aligned; norm rows are padded to a multiple of 64
+// elements (a vector or dword past n stays inside the row; its values are never used).
+//  * With `trow` (SCORE's per-tile maxima of this row, score_tile) and the default pooling kernel
+//    5 (or none): no block barrier and no scores round trip -- every wave reduces the tile
+//    maxima to `max(norms)` itself, and each thread forms the scores of its 8 positions and the
+//    two on either side (a 16-B load of its norms and two 4-B halo loads) in registers, pools
+//    them and writes its keys AND its index vector (returns true: idx is initialised).
+//  * Otherwise (rounds 2-5 form): the row's norms read once as 16-B vectors (kept in registers
+//    for the max and the scores), a block max, scores stored to `tmp` as 16-B vectors, and each
+//    thread pooling 8 positions from three 16-B reads of them (kernel 5; other kernels one
+//    position at a time as snapkv_keys).  Returns false: the caller initialises idx (tmp
+//    aliases it).
 template <int DT, int NT, int MAXV>
-__device__ __forceinline__ void snapkv_keys16(const char* nrow, int n, int pool_k, bool desc, uint16_t* key,
-                              uint16_t* tmp, SelScalars<uint16_t>& sc,
-                              uint64_t* stamps = nullptr) {
+__device__ __forceinline__ bool snapkv_keys16(const char* nrow, const uint32_t* trow, int n,
+                                              int pool_k, bool desc, uint16_t* key, uint16_t* idx,
+                                              uint16_t* tmp, SelScalars<uint16_t>& sc,
+                                              uint64_t* stamps = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nvec = (n + 7) >> 3;
   constexpr uint32_t kInf = DT == KVC_BF16 ? 0x7F80u : 0x7C00u;
+  const bool pool = pool_k > 1 && n >= pool_k;
+  if (trow && (pool_k == 5 || !pool)) {
+    // max(norms) from the tile maxima (bits of the stored norms, at most 256 tiles: <= 4 loads
+    // per lane), one wave reduction; a NaN's bits exceed +inf's.  (Issuing every norm load
+    // before this reduction measured the same: profiles/r06_b_snapkv_ab.jsonl, snap2.)
+    uint32_t mb = 0;
+    const int nt = (n + kTile - 1) / kTile;
+    for (int t = lane; t < nt; t += 64) mb = max(mb, trow[t]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mb = max(mb, (uint32_t)__shfl_xor((int)mb, o, 64));
+    const float mx = mb > kInf ? __builtin_nanf("") : in16<DT>(mb);
+    // `max + 1e-6` (snapkv_lite.py:99): the python scalar takes the tensor's dtype first
+    const float m = in16<DT>(out16<DT>(mx + in16<DT>(out16<DT>(1e-6f))));
+    KVC_STAMP(26);
+    const uint32_t* nw = reinterpret_cast<const uint32_t*>(nrow);
+#pragma unroll
+    for (int q = 0; q < MAXV; ++q) {
+      const int v = tid + q * NT;
+      if (v >= nvec) continue;
+      const uint4 c = reinterpret_cast<const uint4*>(nrow)[v];
+      const uint32_t wp = v > 0 ? nw[4 * v - 1] : 0u;          // positions 8v-2, 8v-1
+      const uint32_t wn = v + 1 < nvec ? nw[4 * v + 4] : 0u;   // positions 8v+8, 8v+9
+      const uint32_t sc6[6] = {snapkv_score_pair<DT>(m, wp), snapkv_score_pair<DT>(m, c.x),
+                               snapkv_score_pair<DT>(m, c.y), snapkv_score_pair<DT>(m, c.z),
+                               snapkv_score_pair<DT>(m, c.w), snapkv_score_pair<DT>(m, wn)};
+      float sw[24];
+#pragma unroll
+      for (int e = 0; e < 24; ++e) sw[e] = 0.f;
+#pragma unroll
+      for (int d = 0; d < 6; ++d) {  // scores of positions 8v - 2 + 2d, +1 at sw[6 + 2d], +1
+        sw[6 + 2 * d] = in16<DT>(sc6[d] & 0xFFFFu);
+        sw[7 + 2 * d] = in16<DT>(sc6[d] >> 16);
+      }
+      reinterpret_cast<uint4*>(key)[v] = snapkv_pool_vec<DT>(sw, v, n, pool, desc);
+      const uint32_t b = (uint32_t)v * 8;
+      reinterpret_cast<uint4*>(idx)[v] =
+          make_uint4(b | (b + 1) << 16, (b + 2) | (b + 3) << 16, (b + 4) | (b + 5) << 16,
+                     (b + 6) | (b + 7) << 16);
+    }
+    KVC_STAMP(29);
+    return true;
+  }
   uint4 raw[MAXV];
   float mx = -__builtin_huge_valf();
   // Branch-free local max: the NaN-ignoring float max (v_max_f32) of every element, NaN
@@ -584,26 +741,14 @@ __device__ __forceinline__ void snapkv_keys16(const char* nrow, int n, int pool_
     uint32_t o[4];
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
-      uint32_t pk = 0;
-      if constexpr (DT == KVC_BF16) {  // one hardware convert per pair (NaN payloads unobserved)
-        pk = f32x2_to_bf16x2_hw(m - bf16_to_f32(w[h]), m - bits_to_f32(w[h] & 0xFFFF0000u));
-        const int i0 = v * 8 + 2 * h;
-        pk &= (i0 + 1 < n ? 0xFFFFFFFFu : i0 < n ? 0x0000FFFFu : 0u);
-      } else {
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const uint32_t u = (w[h] >> (16 * b)) & 0xFFFFu;
-          const float f = in16<DT>(u);
-          pk |= (v * 8 + 2 * h + b < n ? out16<DT>(m - f) : 0u) << (16 * b);
-        }
-      }
-      o[h] = pk;
+      const int i0 = v * 8 + 2 * h;
+      o[h] = snapkv_score_pair<DT>(m, w[h]) &
+             (i0 + 1 < n ? 0xFFFFFFFFu : i0 < n ? 0x0000FFFFu : 0u);
     }
     reinterpret_cast<uint4*>(tmp)[v] = make_uint4(o[0], o[1], o[2], o[3]);
   }
   __syncthreads();
   KVC_STAMP(28);
-  const bool pool = pool_k > 1 && n >= pool_k;
   if (pool && pool_k != 5) {  // other kernels: one position at a time (snapkv_keys)
     const int pad = pool_k / 2;
     for (int i = tid; i < n; i += NT) {
@@ -616,7 +761,7 @@ __device__ __forceinline__ void snapkv_keys16(const char* nrow, int n, int pool_
       for (int j = hs; j < he; ++j) sum = sum + in16<DT>(tmp[j]);
       key[i] = key16_dt<DT>(out16<DT>(sum / (float)psize), desc);
     }
-    return;
+    return false;
   }
   const uint4* tv = reinterpret_cast<const uint4*>(tmp);
 #pragma unroll
@@ -636,74 +781,10 @@ __device__ __forceinline__ void snapkv_keys16(const char* nrow, int n, int pool_
         sw[c * 8 + e] = in16<DT>(u);
       }
     }
-    uint32_t o[4] = {0, 0, 0, 0};
-    if constexpr (DT == KVC_BF16) {
-      // bf16: pairs of positions with packed fp32 adds, one hardware convert and one packed key
-      // map per pair (key_bf16x2 codes for every key of the row).  The window sums drop
-      // avg_pool1d's leading 0 + s: it only turns a -0 into +0, and the keys equate the two.
-      typedef float f2 __attribute__((ext_vector_type(2)));
-      const bool inner = pool && v >= 1 && v * 8 + 10 <= n;  // every window of the vector whole
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        f2 r;
-        if (inner) {
-          f2 acc = f2{sw[2 * p + 6], sw[2 * p + 7]};
-#pragma unroll
-          for (int t = 1; t < 5; ++t) acc = acc + f2{sw[2 * p + 6 + t], sw[2 * p + 7 + t]};
-          r = f2{div5_rn(acc.x), div5_rn(acc.y)};
-        } else {
-#pragma unroll
-          for (int b = 0; b < 2; ++b) {
-            const int e = 2 * p + b, i = v * 8 + e;
-            float x = sw[8 + e];
-            if (pool) {  // pool_k == 5, pad 2: window [i - 2, i + 3) clipped to [0, n), / 5
-              int hs = i - 2;
-              int he = min(hs + 5, n + 2);
-              const int psize = he - hs;
-              hs = max(hs, 0);
-              he = min(he, n);
-              float sum = 0.f;
-#pragma unroll
-              for (int t = 0; t < 5; ++t) {
-                const int j = i - 2 + t;
-                if (j >= hs && j < he) sum = sum + sw[8 + e - 2 + t];
-              }
-              x = psize == 5 ? div5_rn(sum) : sum / (float)psize;
-            }
-            r[b] = x;
-          }
-        }
-        const int i0 = v * 8 + 2 * p;
-        o[p] = key_bf16x2(f32x2_to_bf16x2_hw(r.x, r.y), desc) &
-               (i0 + 1 < n ? 0xFFFFFFFFu : i0 < n ? 0x0000FFFFu : 0u);
-      }
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int i = v * 8 + e;
-        float r;
-        if (pool) {  // pool_k == 5, pad 2: window [i - 2, i + 3) clipped to [0, n), / 5
-          int hs = i - 2;
-          int he = min(hs + 5, n + 2);
-          const int psize = he - hs;
-          hs = max(hs, 0);
-          he = min(he, n);
-          float sum = 0.f;
-#pragma unroll
-          for (int t = 0; t < 5; ++t) {
-            const int j = i - 2 + t;
-            if (j >= hs && j < he) sum = sum + sw[8 + e - 2 + t];
-          }
-          r = psize == 5 ? div5_rn(sum) : sum / (float)psize;
-        } else {
-          r = sw[8 + e];
-        }
-        o[e >> 1] |= (i < n ? (uint32_t)key16_dt<DT>(out16<DT>(r), desc) : 0u) << (16 * (e & 1));
-      }
-    }
-    reinterpret_cast<uint4*>(key)[v] = make_uint4(o[0], o[1], o[2], o[3]);
+    reinterpret_cast<uint4*>(key)[v] = snapkv_pool_vec<DT>(sw, v, n, pool, desc);
   }
   KVC_STAMP(29);
+  return false;
 }
 
 template <int NT>
@@ -2061,7 +2142,9 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
                             int algo, const char* __restrict__ nrow, int32_t* out, uint16_t* sel,
                             char* arrays, int n_cap, int cap,
                             SelScalars<typename DTypeTraits<KC>::key_t>& sc,
-                            int wave_seg, uint64_t* stamps, uint32_t* status) {
+                            int wave_seg, uint64_t* stamps, uint32_t* status,
+                            const uint32_t* trow = nullptr, const char* pf_k = nullptr,
+                            const char* pf_v = nullptr, int pf_rowb = 0) {
   typedef typename DTypeTraits<KC>::key_t KeyT;
   constexpr int ESZ = DTypeTraits<KC>::esz;
   constexpr int MAXJ = (MAXN + NT - 1) / NT;  // positions per lane, level 0
@@ -2097,17 +2180,20 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
     char* tmp = reinterpret_cast<char*>(idx);
     if constexpr (ESZ == 2 && MAXN <= kZoneMax) {
       constexpr int MAXV = (MAXN / 8 + NT - 1) / NT;
+      bool idx_done = false;
       with_dt<KC>(dt, [&](auto D) {
-        snapkv_keys16<D.value, NT, MAXV>(nrow, n, ly->pool_kernel, desc,
-                                         reinterpret_cast<uint16_t*>(key),
-                                         reinterpret_cast<uint16_t*>(tmp), sc, stamps);
+        idx_done = snapkv_keys16<D.value, NT, MAXV>(nrow, trow, n, ly->pool_kernel, desc,
+                                                    reinterpret_cast<uint16_t*>(key), idx,
+                                                    reinterpret_cast<uint16_t*>(tmp), sc, stamps);
       });
-      __syncthreads();  // the scores (in the idx region) are dead
-      for (int v = tid; v < (n + 7) / 8; v += NT) {
-        const uint32_t b = (uint32_t)v * 8;
-        reinterpret_cast<uint4*>(idx)[v] =
-            make_uint4(b | (b + 1) << 16, (b + 2) | (b + 3) << 16, (b + 4) | (b + 5) << 16,
-                       (b + 6) | (b + 7) << 16);
+      if (!idx_done) {
+        __syncthreads();  // the scores (in the idx region) are dead
+        for (int v = tid; v < (n + 7) / 8; v += NT) {
+          const uint32_t b = (uint32_t)v * 8;
+          reinterpret_cast<uint4*>(idx)[v] =
+              make_uint4(b | (b + 1) << 16, (b + 2) | (b + 3) << 16, (b + 4) | (b + 5) << 16,
+                         (b + 6) | (b + 7) << 16);
+        }
       }
     } else {
       with_dt<KC>(dt, [&](auto D) {
@@ -2225,6 +2311,20 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
     if (st == 1 && wid == 0)
       run_chain<KeyT, 64, 16>(key, idx, spos, A.gpos, sc, k, topk, thr, cap, lo, hi, depth,
                               level, wave_seg, accw, status);
+    if constexpr (kSgPrefetch && TO_LDS && NT > 64) {
+      // while wave 0 finishes the chain, the other waves touch the K / V rows of the positions
+      // already known to be kept (idx[0, lo): stable, wave 0 only rearranges [lo, hi)), so that
+      // the row's copy finds them in the caches (diagnostic A/B: KVC_SG_PREFETCH)
+      if (st == 1 && wid > 0 && pf_rowb > 0) {
+        const int64_t kss = ly->k_stride[2] * ESZ, vss = ly->v_stride[2] * ESZ;
+        for (int u = tid - 64; u < lo * 4; u += NT - 64) {
+          const int p = ly->zone_start + (int)idx[u >> 2];
+          const char* a = ((u & 2) ? pf_v + p * vss : pf_k + p * kss) + ((u & 1) ? pf_rowb - 4 : 0);
+          const uint32_t x = *reinterpret_cast<const volatile uint32_t*>(a);
+          asm volatile("" ::"v"(x));
+        }
+      }
+    }
   }
   __syncthreads();
   KVC_STAMP(3);
@@ -2282,26 +2382,27 @@ __global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT, HH))
     select_kernel(const LayerChunk T, int BH, int dt, int order, int algo,
                   const char* __restrict__ norms, int64_t norm_stride,
                   int32_t* __restrict__ out_idx, int64_t idx_stride, int wave_seg, int n_cap,
-                  int cap, uint64_t* stamps, uint32_t* status) {
+                  int cap, uint64_t* stamps, uint32_t* status, const uint32_t* __restrict__ tmax) {
   typedef typename DTypeTraits<KC>::key_t KeyT;
   constexpr int ESZ = DTypeTraits<KC>::esz;
   constexpr int MAXN = NT == kSelThreads ? kZoneMax : NT * 16;
   __shared__ SelScalars<KeyT> sc;
   const kvc_layer_t* ly = T.l + blockIdx.x / BH;
   const int row = ly->row0 + (int)(blockIdx.x % BH);  // global workspace row
+  const uint32_t* trow = tmax ? tmax + (int64_t)row * (norm_stride / kTile) : nullptr;
   if constexpr (NT == kSelThreads) {
     // LDS: key[kZoneMax] | idx[kZoneMax] (u16) | spos | gpos (u16 rank windows) -- SelArrays
     __shared__ __attribute__((aligned(16))) char smem[kSelBytesBig<KeyT>];
     select_body<KC, false, MAXN, NT, HH, STABLE>(ly, dt, order, algo,
                                      norms + (int64_t)row * norm_stride * ESZ,
                                      out_idx + (int64_t)row * idx_stride, nullptr, smem, kZoneMax,
-                                     kSelCapBig<KeyT>, sc, wave_seg, stamps, status);
+                                     kSelCapBig<KeyT>, sc, wave_seg, stamps, status, trow);
   } else {
     extern __shared__ __attribute__((aligned(16))) char dsmem[];
     select_body<KC, false, MAXN, NT, HH, STABLE>(ly, dt, order, algo,
                                      norms + (int64_t)row * norm_stride * ESZ,
                                      out_idx + (int64_t)row * idx_stride, nullptr, dsmem, n_cap,
-                                     cap, sc, wave_seg, stamps, status);
+                                     cap, sc, wave_seg, stamps, status, trow);
   }
 }
 
@@ -2758,7 +2859,8 @@ template <int KC, int NT, int NC, bool STABLE = false>
 __global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT))
     select_gather_kernel(const LayerChunk T, int H, int BH, int dt, int order, int algo,
                          const char* __restrict__ norms, int64_t norm_stride, int wave_seg,
-                         int n_cap, int cap, uint32_t* status, int split_rows) {
+                         int n_cap, int cap, uint32_t* status, int split_rows,
+                         const uint32_t* __restrict__ tmax) {
   typedef typename DTypeTraits<KC>::key_t KeyT;
   constexpr int ESZ = DTypeTraits<KC>::esz;
   constexpr int MAXN = NT == kSelThreads ? kZoneMax : NT * 16;
@@ -2798,10 +2900,17 @@ __global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT))
   // its keys to the end: the idx region then)
   uint16_t* sel = reinterpret_cast<uint16_t*>(arrays + (STABLE ? (size_t)n_cap * sizeof(KeyT) : 0));
   if (selects) {
+    const uint32_t* trow =
+        tmax ? tmax + (int64_t)(ly->row0 + r) * (norm_stride / kTile) : nullptr;
+    const int b = r / H, h = r - (r / H) * H;
+    const char* pk = static_cast<const char*>(ly->k) +
+                     ((int64_t)b * ly->k_stride[0] + (int64_t)h * ly->k_stride[1]) * ESZ;
+    const char* pv = static_cast<const char*>(ly->v) +
+                     ((int64_t)b * ly->v_stride[0] + (int64_t)h * ly->v_stride[1]) * ESZ;
     const bool ok = select_body<KC, true, MAXN, NT, false, STABLE>(ly, dt, order, algo, nrow,
                                                                   nullptr, sel,
                                                     arrays, n_cap, cap, sc, wave_seg, nullptr,
-                                                    status);
+                                                    status, trow, pk, pv, NC * 16);
     if (!ok) return;  // flagged in *status; the row's output is left unwritten (the copier
                       // workgroup of a split row skips it too)
     __syncthreads();
@@ -3110,6 +3219,7 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
   const int64_t BH = (int64_t)p->batch * p->heads;
   if (BH * nl > 0x7FFFFFFF) return KVC_E_ARG;
   int64_t tiles = 0, units = 0, max_zone = 0, max_sel = 0;
+  bool snap = false;  // a snapkv row is scored: the per-tile maxima region
   for (int l = 0; l < nl; ++l) {
     kvc_layer_t& y = layers[l];
     const int S = y.seq_len;
@@ -3148,6 +3258,7 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
       return KVC_E_ARG;
     }
     if (needs_select && y.zone_len > max_zone) max_zone = y.zone_len;
+    snap |= needs_select && y.score_mode == KVC_SCORE_SNAPKV;
     if (y.n_select > max_sel) max_sel = y.n_select;
     tiles += tl;
     units += ul;
@@ -3167,12 +3278,23 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
     off = round_up(off + (size_t)rows * info->index_row_stride * 4, 256);
     if (max_zone > kZoneMax)  // selection scratch rows for zones longer than the LDS limit
       off += (size_t)rows * sel_scratch_row_bytes((int)info->norm_row_stride, p->dtype);
+    // snapkv rows: SCORE's per-64-token-tile norm maxima (u32 each; tmax_offset())
+    if (snap) off += (size_t)rows * (size_t)(info->norm_row_stride / kTile) * 4;
 #ifdef KVC_STAMPS
     off += (size_t)rows * 256;  // diagnostic stamp slots (32 x u64 per select row)
 #endif
     info->workspace_bytes = off;
   }
   return KVC_OK;
+}
+
+// Offset of the snapkv per-tile maxima region (rows x norm_row_stride / 64 u32): after the index
+// region and the long-zone selection scratch (plan_impl's layout).
+static inline size_t tmax_offset(const kvc_plan_info_t& info, int dtype) {
+  size_t off = round_up(info.index_offset + (size_t)info.rows * info.index_row_stride * 4, 256);
+  if (info.norm_row_stride > kZoneMax)
+    off += (size_t)info.rows * sel_scratch_row_bytes((int)info.norm_row_stride, dtype);
+  return off;
 }
 
 // Every launch goes through hipLaunchKernel, whose return value is this launch's own status (a
@@ -3216,11 +3338,12 @@ static int with_nc(int nc, F&& f) {
 // would otherwise evict useful lines from the Infinity Cache.
 template <int DT, int NC>
 static int launch_score(const LayerChunk& T, int nl, int H, int64_t tile_base,
-                        int64_t chunk_tiles, char* norms, int64_t nstride, hipStream_t s) {
+                        int64_t chunk_tiles, char* norms, int64_t nstride, uint32_t* tmax,
+                        hipStream_t s) {
   constexpr int per_wg = score_waves(NC);  // one tile per wave
   const unsigned grid = (unsigned)((chunk_tiles + per_wg - 1) / per_wg);
   return launch_k(score_kernel<DT, NC, true>, dim3(grid), dim3(per_wg * 64), 0, s, T, nl, H,
-                  tile_base, chunk_tiles, norms, nstride);
+                  tile_base, chunk_tiles, norms, nstride, tmax, nstride / kTile);
 }
 
 // `work` = max n_out over the chunk's layers; grid = (rows, token blocks)
@@ -3251,7 +3374,7 @@ template <int KC, bool HH = false>
 static int launch_select(const LayerChunk& T, int cn, int BH, int dt, int order, int algo,
                          const char* norms, int64_t nstride, int32_t* idx, int64_t istride,
                          bool long_zone, char* scratch, uint64_t* stamps, uint32_t* status,
-                         hipStream_t s) {
+                         hipStream_t s, const uint32_t* tmax = nullptr) {
   typedef typename DTypeTraits<KC>::key_t KeyT;
   const dim3 rows_grid((unsigned)(cn * BH));
   const int n_cap = (int)nstride;  // longest zone of the call, rounded to 64
@@ -3275,11 +3398,12 @@ static int launch_select(const LayerChunk& T, int cn, int BH, int dt, int order,
       const int cap = sel_cap(n_cap, ks, kSmallBudget);
       return launch_k(select_kernel<KC, kSelThreadsSmall, HH, ST>, rows_grid,
                       dim3(kSelThreadsSmall), sel_bytes(n_cap, ks, cap), s, T, BH, dt, order, algo,
-                      norms, nstride, idx, istride, kWaveSegSmall, n_cap, cap, stamps, status);
+                      norms, nstride, idx, istride, kWaveSegSmall, n_cap, cap, stamps, status,
+                      tmax);
     }
     return launch_k(select_kernel<KC, kSelThreads, HH, ST>, rows_grid, dim3(kSelThreads), 0, s, T,
                     BH, dt, order, algo, norms, nstride, idx, istride, kWaveSeg, n_cap, 0, stamps,
-                    status);
+                    status, tmax);
   };
   if (algo == KVC_ALGO_STABLE) return go(std::true_type());
   return go(std::false_type());
@@ -3309,10 +3433,11 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
   const int part = (p->flags & KVC_FLAG_GATHER_FIXED)      ? PART_FIXED
                    : (p->flags & KVC_FLAG_GATHER_SELECTED) ? PART_SELECTED
                                                            : PART_ALL;
-  bool sel = false, long_zone = false;
+  bool sel = false, long_zone = false, snap = false;
   int64_t max_out = 0, max_part = 0;
   for (int l = c0; l < c0 + cn; ++l) {
     sel |= layers[l].n_select > 0;
+    snap |= layer_selects(layers[l]) && layers[l].score_mode == KVC_SCORE_SNAPKV;
     long_zone |= layer_selects(layers[l]) && layers[l].zone_len > kZoneMax;
     max_out = layers[l].n_out > max_out ? layers[l].n_out : max_out;
     const int64_t pr = part_rows(layers[l], part);
@@ -3320,9 +3445,12 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
   }
   const bool ext = p->external_index != 0;
   uint32_t* status = p->device_status;
+  // snapkv rows: SCORE's per-tile norm maxima (plan_impl reserved them), read by the selection
+  uint32_t* tmax = snap && !ext ? reinterpret_cast<uint32_t*>(w + tmax_offset(info, p->dtype))
+                                : nullptr;
   int rc = KVC_OK;
   if ((p->phases & KVC_PHASE_SCORE) && tile_end > tile_base && !ext)
-    rc = launch_score<DT, NC>(T, cn, H, tile_base, tile_end - tile_base, norms, nstride, s);
+    rc = launch_score<DT, NC>(T, cn, H, tile_base, tile_end - tile_base, norms, nstride, tmax, s);
   if (rc != KVC_OK) return rc;
   const int n_cap = (int)nstride;  // longest zone of the call, rounded to 64
   if ((p->phases & KVC_PHASE_SELECT) && sel && !ext) {
@@ -3339,7 +3467,8 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
           const int cap = sel_cap(n_cap, ks, kSmallBudget);
           return launch_k(select_gather_kernel<KC, kSelThreadsSmall, NC, ST>, rows_grid,
                           dim3(kSelThreadsSmall), sel_bytes(n_cap, ks, cap), s, T, H, BH, DT,
-                          p->order, p->algo, norms, nstride, kWaveSegSmall, n_cap, cap, status, 0);
+                          p->order, p->algo, norms, nstride, kWaveSegSmall, n_cap, cap, status, 0,
+                          tmax);
         }
         // fewer rows than CUs (e.g. 4 layers per GPU of an 8-way layer split): one row per CU
         // and idle CUs -- the sink / tail rows get copy-only workgroups of their own
@@ -3350,14 +3479,14 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
         return launch_k(select_gather_kernel<KC, kSelThreads, NC, ST>,
                         dim3((unsigned)(split ? 2 * rows : rows)), dim3(kSelThreads), 0, s, T, H,
                         BH, DT, p->order, p->algo, norms, nstride, kWaveSeg, n_cap, 0, status,
-                        split);
+                        split, tmax);
       };
       return p->algo == KVC_ALGO_STABLE ? go(std::true_type()) : go(std::false_type());
     }
     char* scratch = w + round_up(info.index_offset + (size_t)info.rows * istride * 4, 256);
     uint64_t* st = stamps ? stamps + (size_t)layers[c0].row0 * 32 : nullptr;
     rc = launch_select<KC>(T, cn, BH, DT, p->order, p->algo, norms, nstride, idx, istride,
-                           long_zone, scratch, st, status, s);
+                           long_zone, scratch, st, status, s, tmax);
   }
   if (rc != KVC_OK) return rc;
   if ((p->phases & KVC_PHASE_GATHER) && max_part > 0)
@@ -3396,11 +3525,13 @@ static int debug_select_impl(const kvc_params_t* p, const kvc_layer_t* layers, i
       return launch_k(select_kernel<KC, kSelThreadsSmall>, grid, dim3(kSelThreadsSmall), lds, s,
                       T, BH, DT, p->order, p->algo, norms, info.norm_row_stride, idx,
                       info.index_row_stride, kWaveSegSmall, zone_cap, cap,
-                      static_cast<uint64_t*>(nullptr), p->device_status);
+                      static_cast<uint64_t*>(nullptr), p->device_status,
+                      static_cast<const uint32_t*>(nullptr));
     return with_nc(nc, [&](auto ncv) {
       return launch_k(select_gather_kernel<KC, kSelThreadsSmall, decltype(ncv)::value>, grid,
                       dim3(kSelThreadsSmall), lds, s, T, H, BH, DT, p->order, p->algo, norms,
-                      info.norm_row_stride, kWaveSegSmall, zone_cap, cap, p->device_status, 0);
+                      info.norm_row_stride, kWaveSegSmall, zone_cap, cap, p->device_status, 0,
+                      static_cast<const uint32_t*>(nullptr));
     });
   });
 }

@@ -22,13 +22,16 @@ rounding is host-dependent: the tests that replay these runs skip on another CPU
 (tests/golden/step_digest.py: a digest of the call's input keys and of the positions it kept,
 recovered from position-encoding values), so that another host can check the engine's
 selections against the reference's at every step where its forward reproduces the keys, and
-name the first step where it does not.
+name the first step where it does not; and for the snapkv_lite and l2_compress runs every K
+row the model appended is kept (eval_loop_rows.npz), which replays their compress calls on the
+reference's exact inputs on any host (step_digest.replay).
 """
 import importlib.util
 import json
 import os
 import sys
 
+import numpy as np
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -38,6 +41,11 @@ THREADS = 8
 MAX_TOKENS = 700
 KW = dict(start_size=4, heavy_hitter_size=16, recent_size=40)
 FIELDS = ("perplexity", "accuracy", "num_tokens", "final_cache_size")
+# the method runs whose every appended K row is kept (eval_loop_rows.npz), so that another host
+# can replay their compress calls on the reference's exact keys (step_digest.replay): layers 1-2
+# (layer 0 is skipped by every run, and passed through untouched)
+ROW_METHODS = ("snapkv_lite", "l2_compress")
+ROW_LAYERS = (1, 2)
 
 
 def cpu_model():
@@ -102,18 +110,25 @@ def main():
     from kvcompress.methods import get_compress_fn
     from test_ppl_parity import CASES
     methods = []
+    rows = {}
     for name, kw in CASES:
         rec = Recorder(get_compress_fn(name))
+        if name in ROW_METHODS:
+            rec.new_rows(ROW_LAYERS)
         r = R_eval.evaluate_with_compression(model, tok, text, compress_fn=rec,
                                              compress_kwargs=kw, max_tokens=MAX_TOKENS,
                                              skip_layers=[0], show_progress=False)
         methods.append({"name": name, "kwargs": kw, **{f: r[f] for f in FIELDS},
                         "steps": rec.packed()})
+        if name in ROW_METHODS:
+            rows[name] = np.stack(rec.rows)
     out = {"threads": THREADS, "max_tokens": MAX_TOKENS, "kw": KW, "layers": 3,
            "cpu_model": cpu_model(), "cpu_capability": torch.backends.cpu.get_cpu_capability(),
            "text": "TEXT * 2", "runs": {k: {f: v[f] for f in FIELDS} for k, v in runs.items()},
            "methods": methods, "steps": steps}
     json.dump(out, open(os.path.join(HERE, "eval_attention.json"), "w"), indent=1)
+    np.savez_compressed(os.path.join(HERE, "eval_loop_rows.npz"),
+                        **{f"{k}_rows": v for k, v in rows.items()})
     print(json.dumps(out["runs"]), json.dumps([{f: m[f] for f in FIELDS} for m in methods]))
 
 

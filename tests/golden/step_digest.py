@@ -54,11 +54,22 @@ class Recorder:
     def __call__(self, kv_list, **kw):
         kv_list = list(kv_list)
         kd = k_digest(kv_list)
+        if getattr(self, "rows", None) is not None:
+            self.rows.append(np.stack([_np32(kv_list[l][0][:, :, -1:, :])
+                                       for l in self.row_layers]))
         enc = [(k, torch.from_numpy(prng.encode_positions(tuple(v.shape), "fp32")).to(v.dtype))
                for k, v in kv_list]
         pd = pos_digest(self.fn(enc, **kw))
         self.steps.append((kd, pd))
         return self.fn(kv_list, **kw)
+
+    def new_rows(self, layers):
+        """Keep, from every call, the last K row of each of `layers` (the token the model
+        appended since the previous call): with the first call's cache, enough to replay every
+        call's input without the model (replay)."""
+        self.row_layers = list(layers)
+        self.rows = []
+        return self
 
     def packed(self):
         """The record as one string, 'kd:pd' per call, comma-separated."""
@@ -80,3 +91,27 @@ def first_divergence(got, ref):
         if got[i][1] != ref[i][1]:
             bad.append(i)
     return n, None, bad
+
+
+def replay(fn, rows, n_layers, row_layers, kwargs, steps=None):
+    """Re-run a recorded loop's compress calls without its model: the cache starts empty and
+    every call appends one row per layer -- the recorded K row for `row_layers` (`rows`:
+    [calls, len(row_layers), B, H, 1, D] float32), zeros for the others, which must be layers
+    the calls pass through untouched (skip_layers) -- then compresses with fn, values encoding
+    positions.  The next call continues from fn's output, as the loop did.  Returns the
+    position digests per call (the `pd` of a Recorder record)."""
+    B, H, D = rows.shape[2], rows.shape[3], rows.shape[5]
+    ks = [torch.zeros(B, H, 0, D) for _ in range(n_layers)]
+    out = []
+    for t in range(rows.shape[0] if steps is None else steps):
+        kv = []
+        for l in range(n_layers):
+            new = (torch.from_numpy(rows[t, row_layers.index(l)]) if l in row_layers
+                   else torch.zeros(B, H, 1, D))
+            k = torch.cat([ks[l], new], dim=2)
+            v = torch.from_numpy(prng.encode_positions(tuple(k.shape), "fp32"))
+            kv.append((k, v))
+        res = fn(kv, **kwargs)
+        out.append(pos_digest(res))
+        ks = [r[0].detach().to("cpu", torch.float32) for r in res]
+    return out

@@ -14,7 +14,7 @@ import torch
 
 from gpu_util import to_dev, to_np
 from oracle import h2o_oracle as HO
-from step_digest import Recorder, first_divergence, unpack
+from step_digest import Recorder, first_divergence, replay, unpack
 from test_ppl_parity import TEXT, ToyTokenizer, gqa_model, toy_model
 
 KW = dict(start_size=4, heavy_hitter_size=16, recent_size=40)
@@ -362,4 +362,43 @@ def test_engine_loop_selections_match_reference_steps():
             with open(path, "w") as f:
                 json.dump(report, f, indent=1)
         print(json.dumps(report))
+    assert _engine.device_status(0) == 0
+
+
+def _rows():
+    import os
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", "eval_loop_rows.npz"))
+
+
+def _replay_case(name, fn):
+    from gen_eval_attention import ROW_LAYERS
+    gold = _gold()
+    ref = next(m for m in gold["methods"] if m["name"] == name)
+    kw = dict(ref["kwargs"], skip_layers=[0])
+    got = replay(fn, _rows()[f"{name}_rows"], gold["layers"], ROW_LAYERS, kw)
+    want = [pd for _, pd in unpack(ref["steps"])]
+    assert len(got) == len(want) == gold["max_tokens"] - 1
+    return got, want
+
+
+@pytest.mark.parametrize("name", ["snapkv_lite", "l2_compress"])
+def test_oracle_replays_reference_loop_selections(name):
+    """Host-independent: the reference loop's compress calls re-run from its recorded K rows
+    (eval_loop_rows.npz, no model forward) with the oracle keep, at every one of the 699 steps,
+    the positions the reference kept."""
+    from test_ppl_parity import oracle_compress as oracle_method
+    got, want = _replay_case(name, oracle_method(name))
+    assert got == want, [i for i, (a, b) in enumerate(zip(got, want)) if a != b][:5]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["snapkv_lite", "l2_compress"])
+def test_engine_replays_reference_loop_selections(name):
+    """The same replay with every compress call on the HIP engine: the engine keeps the
+    reference's positions at all 699 steps of the loop whose perplexity differs on the GPU box's
+    CPU (its forward rounds the first token's keys differently:
+    test_engine_loop_selections_match_reference_steps reports step 0 as the first divergence)."""
+    from kvcompress import _engine
+    got, want = _replay_case(name, _engine_bridge(name))
+    assert got == want, [i for i, (a, b) in enumerate(zip(got, want)) if a != b][:5]
     assert _engine.device_status(0) == 0

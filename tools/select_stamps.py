@@ -93,10 +93,16 @@ if os.environ.get("SEL_P1_STAMPS"):  # diagnostic: level-0 P1 sub-phases (slots 
             ("wave_start_skew", "longest_wave_P1", "last_P1_end_after_first_start",
              "last_P2_end_after_B_a"))}}))
 if os.environ.get("SEL_SNAP_STAMPS"):  # diagnostic: snapkv scoring phases (slots 26..29)
-    sn = allst[:, [1 - 1 + 1, 26, 27, 28, 29]]
-    ph = np.stack([allst[:, 26] - allst[:, 0], allst[:, 27] - allst[:, 26],
-                   allst[:, 28] - allst[:, 27], allst[:, 29] - allst[:, 28],
-                   allst[:, 1] - allst[:, 29]], axis=1)
-    print(json.dumps({"snapkv_phases_median": [float(np.median(ph[:, i])) for i in range(5)],
-                      "names": ["load+local max", "block max", "scores->tmp", "pool+keys",
-                                "idx init"]}))
+    if np.all(allst[:, 27] == 0):  # round 6: SCORE's tile maxima, no block barrier / tmp
+        ph = np.stack([allst[:, 26] - allst[:, 0], allst[:, 29] - allst[:, 26],
+                       allst[:, 1] - allst[:, 29], allst[:, 1] - allst[:, 0]], axis=1)
+        names = ["tile max -> m", "scores+pool+keys+idx (halo loads)", "barrier",
+                 "snapkv scoring total"]
+    else:
+        ph = np.stack([allst[:, 26] - allst[:, 0], allst[:, 27] - allst[:, 26],
+                       allst[:, 28] - allst[:, 27], allst[:, 29] - allst[:, 28],
+                       allst[:, 1] - allst[:, 29], allst[:, 1] - allst[:, 0]], axis=1)
+        names = ["load+local max", "block max", "scores->tmp", "pool+keys", "idx init",
+                 "snapkv scoring total"]
+    print(json.dumps({"snapkv_phases_median": [float(np.median(ph[:, i])) for i in range(len(names))],
+                      "names": names}))
