@@ -101,7 +101,7 @@ def job_bytes(jobs, es):
     return {"path": path, "score": score, "select+gather": gather}
 
 
-PMC_FILE = "profiles/r05_z_pmc_traffic.json"  # tools/pmc_round.sh (tools/gpu.sh pmc) + tools/pmc_traffic.py
+PMC_FILE = "profiles/r06_z_pmc_traffic.json"  # tools/pmc_round.sh (tools/gpu.sh pmc) + tools/pmc_traffic.py
 
 
 def pmc_traffic(kernel="kvc::score_kernel<1, 16, true>"):
