@@ -568,3 +568,28 @@ def test_abi_tiny_segments_and_adversaries(dtype, mode):
             K[0, 0, :, 0] = (adv[:n] + 1).astype(np.float32)  # exact in bf16 / fp16 (<= 256)
             nrm, idx = _abi_select(prng.to_dtype(K, dtype), k, 0, mode)
             np.testing.assert_array_equal(idx, ref_of(nrm, k), err_msg=f"adversary n={n} k={k}")
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16"])
+@pytest.mark.parametrize("variant", ["special", "equal", "zero", "tiny", "few"])
+def test_snapkv_scoring_from_tile_maxima(dtype, variant, launch_path):
+    """snapkv_lite's row max comes from SCORE's per-64-token-tile norm maxima (bit patterns; a
+    NaN's exceed +inf's) and its scores / pooling from each thread's norms plus a 4-byte halo
+    (round 6, snapkv_keys16): NaN / +-inf / zero / all-equal / sub-normal rows, zones whose last
+    tile is partial or a single position, on the 512-thread (<= 8 192 positions) and the
+    1 024-thread rows, pooling 5 and none, against the oracle; pooling 3 keeps the two-barrier
+    path on the same rows.  Both launch paths."""
+    from kvcompress.methods import snapkv_lite_compress
+    bits = {2: np.uint16, 4: np.uint32}
+    for S, pk in ((8224, 5), (12000, 5), (16384, 5), (8257, 1), (12000, 3), (16353, 5)):
+        shape = (1, 2, S, 64)
+        layers_np = [(prng.gen_keys(9300 + S + i, shape, dtype, variant if i else "special"),
+                      prng.gen_values(9300 + S + i, shape, dtype)) for i in range(2)]
+        tin = [(to_dev(k), to_dev(v)) for k, v in layers_np]
+        kw = dict(observation_window=32, keep_size=1024, pooling_kernel=pk, skip_layers=[])
+        out = snapkv_lite_compress(list(tin), **kw)
+        ref = oracle.snapkv_lite_compress(layers_np, **kw)
+        for li, ((ko, vo), (rk, rv, _)) in enumerate(zip(out, ref)):
+            b = bits[rk.dtype.itemsize]
+            assert np.array_equal(to_np(ko).view(b), rk.view(b)) and \
+                np.array_equal(to_np(vo).view(b), rv.view(b)), (S, pk, li)
