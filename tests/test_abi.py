@@ -280,3 +280,36 @@ def test_heavy_hitter_stable_flag():
     assert N.hh_workspace(p(N.ATTN_HH_STABLE), table(70000))[0] == N.KVC_E_TOO_LONG
     assert N.hh_workspace(p(8), table(15936))[0] == -1  # KVC_E_ARG
     assert N.hh_workspace(p(N.ATTN_OLD_DTYPE(N.KVC_F32)), table(15936))[0] == -1  # accumulate only
+
+
+def test_device_status_bits_match_header():
+    """enum kvc_device_status (include/kvc.h, ABI v4) and the Python side agree, and every bit
+    has a name in the opt-in status check's message table."""
+    from kvcompress import _engine as E
+    hdr = open(os.path.join(ROOT, "include", "kvc.h")).read()
+    vals = dict(re.findall(r"(KVC_DEV_\w+) = (\d+)", hdr))
+    assert vals == {"KVC_DEV_SELECT_BOUNDS": "1", "KVC_DEV_INDEX_RANGE": "2",
+                    "KVC_DEV_INTERNAL": "4"}
+    assert (N.DEV_SELECT_BOUNDS, N.DEV_INDEX_RANGE, N.DEV_INTERNAL) == (1, 2, 4)
+    assert [b for b, _ in E._STATUS_BITS] == [1, 2, 4]
+    assert all(name.split()[0] in vals for _, name in E._STATUS_BITS)
+
+
+def test_snapkv_calls_reserve_the_tile_maxima_region():
+    """kvc_plan reserves rows x norm_row_stride / 64 u32 after the index region when a layer
+    scores with snapkv (SCORE's per-tile norm maxima, round 6), and nothing for plain norms."""
+    H, D = 4, 64
+
+    def plan(mode):
+        t = np.zeros(1, dtype=N.LAYER_DTYPE)
+        t[0]["k"] = t[0]["v"] = t[0]["k_out"] = t[0]["v_out"] = 4096
+        t[0]["k_stride"] = t[0]["v_stride"] = (H * 1000 * D, 1000 * D, D)
+        t[0]["seq_len"], t[0]["zone_start"], t[0]["zone_len"], t[0]["n_select"] = 1000, 0, 968, 480
+        t[0]["score_mode"], t[0]["pool_kernel"] = mode, 5 if mode else 0
+        p = N.Params(dtype=N.KVC_BF16, batch=1, heads=H, head_dim=D, order=1, algo=1,
+                     phases=N.PHASE_ALL, external_index=0)
+        rc, info = N.plan(p, t)
+        assert rc == 0
+        return info
+    a, b = plan(0), plan(1)
+    assert b.workspace_bytes - a.workspace_bytes == b.rows * (b.norm_row_stride // 64) * 4
