@@ -82,6 +82,13 @@ constexpr bool kSgNts = KVC_SG_NTS;
 #define KVC_SG_NTL false
 #endif
 constexpr bool kSgNtl = KVC_SG_NTL;
+// SCORE also derives each plain-norm row's level-0 pivot and writes per-tile ge / le counts
+// (score_tile), which the selection's first partition level sums instead of re-reading the row
+// (partition_level); 0: level 0 counts its keys itself (A/B)
+#ifndef KVC_L0_TILE_COUNTS
+#define KVC_L0_TILE_COUNTS 1
+#endif
+constexpr bool kL0TileCounts = KVC_L0_TILE_COUNTS;
 // SELECT_GATHER rows touch the rows they already know they keep while wave 0 finishes the chain
 // (select_body; diagnostic A/B, off)
 #ifndef KVC_SG_PREFETCH
@@ -363,6 +370,54 @@ __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int t
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) bits = max(bits, (uint32_t)__shfl_xor((int)bits, o, 64));
     if (lane == 0) tmax[(int64_t)(ly->row0 + row) * tmax_stride + tt] = bits;
+  }
+  // Plain-norm rows: level 0's P1 counts, per tile (round 6).  Each wave re-derives the row's
+  // level-0 pivot -- the median of the keys at zone positions 1, n/2, n-1, as
+  // std::__move_median_to_first picks it (partition_level) -- by loading those three token rows
+  // (L2 hits after their first wave) and computing their norms in torch.norm's order, then
+  // counts its tile's keys >= / <= that pivot (ascending keys; a descending selection swaps the
+  // two) and stores ge | le << 16.  Free: the stream is HBM-bound (SCORE 0.6164-0.6194 vs
+  // 0.6164-0.6201 ms, profiles/r06_e_l0_counts_ab.jsonl).
+  if constexpr (kL0TileCounts) if (ly->score_mode == KVC_SCORE_NORM && tmax && zlen > 2) {
+    const int ptok[3] = {1, zlen / 2, zlen - 1};
+    const char* zb = static_cast<const char*>(ly->k) +
+                     ((int64_t)b * ly->k_stride[0] + (int64_t)h * ly->k_stride[1] +
+                      (int64_t)ly->zone_start * ly->k_stride[2]) * ESZ;
+    // token r's chunk c -> slab row r * NPH + c / CP, column c % CP
+    for (int u = lane; u < 3 * NC; u += 64) {
+      const int r = u / NC, c = u - r * NC;
+      const uint4 x = *reinterpret_cast<const uint4*>(zb + ptok[r] * sbytes + c * 16);
+      *reinterpret_cast<uint4*>(wl + (r * NPH + c / CP) * ROWB + (c % CP) * 16) = x;
+    }
+    wave_sync();
+    float pa[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (lane < 3) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        accum_chunk<DT, NC>(pa, *reinterpret_cast<const uint4*>(wl + (lane * NPH + c / CP) * ROWB +
+                                                                 (c % CP) * 16), c);
+    }
+    float ps = pa[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j) ps = ps + pa[j];
+    const float pr = __builtin_sqrtf(ps);
+    uint32_t pk;
+    if constexpr (DT != KVC_F32) pk = key16_dt<DT>(bits16_dt<DT>(pr), false);
+    else pk = key_f32(f32_to_bits(pr), false);
+    const uint32_t ka = (uint32_t)__builtin_amdgcn_readlane((int)pk, 0);
+    const uint32_t kb = (uint32_t)__builtin_amdgcn_readlane((int)pk, 1);
+    const uint32_t kc = (uint32_t)__builtin_amdgcn_readlane((int)pk, 2);
+    const uint32_t p = ka < kb ? (kb < kc ? kb : (ka < kc ? kc : ka))
+                               : (ka < kc ? ka : (kb < kc ? kc : kb));
+    uint32_t mk;
+    if constexpr (DT != KVC_F32) mk = key16_dt<DT>(bits, false);
+    else mk = key_f32(bits, false);
+    const bool in = lane < ntok;
+    const int ge = __popcll(__builtin_amdgcn_ballot_w64(in && mk >= p));
+    const int le = __popcll(__builtin_amdgcn_ballot_w64(in && mk <= p));
+    if (lane == 0)
+      tmax[(int64_t)(ly->row0 + row) * tmax_stride + tt] = (uint32_t)ge | ((uint32_t)le << 16);
+    wave_sync();
   }
 }
 
@@ -1424,7 +1479,8 @@ __device__ __forceinline__ void wave_tiny_chain(KeyT* key, uint16_t* idx, int k,
 template <typename KeyT, int NT, int JM>
 __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_t* spos,
                                                uint16_t* gpos, SelScalars<KeyT>& sc, int lo,
-                                               int hi, int cap, uint64_t* acc) {
+                                               int hi, int cap, uint64_t* acc,
+                                               const uint32_t* tcnt = nullptr, bool desc = false) {
   constexpr int NW = NT / 64;
   typedef typename std::conditional<(JM > 32), uint64_t, uint32_t>::type MaskT;
   const int lane = threadIdx.x & 63;
@@ -1459,7 +1515,35 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
   KVC_TICK(ta);
   // ---- P1: wave ge / le counts ----
   int cge = 0, cle = 0;
-  if (whole)
+  if (tcnt) {
+    // level 0 of a plain-norm row (lo = 0, hi = n): SCORE counted every 64-token tile against
+    // this pivot (score_tile).  This stripe [wbeg, wbeg + 64 J), wbeg = 1 + 64 T0, is tiles
+    // T0 .. T0 + J - 1 without position 64 T0 (the previous stripe's last, or the pivot slot lo)
+    // and with position 64 (T0 + J) (its own last, in the next tile).  Same counts as the pass
+    // below, including slot ch counted with the pivot's key (corrected for the median move).
+    const int T0 = wid * J, nt = (hi + kTile - 1) / kTile;
+    const uint32_t c = lane < J && T0 + lane < nt ? tcnt[T0 + lane] : 0u;
+    const uint32_t sum = (uint32_t)__builtin_amdgcn_readlane(row_scan16((int)c), 15);
+    uint32_t g = sum & 0xFFFFu, l = sum >> 16;
+    if (desc) {  // descending keys are complemented: ge <-> le of the ascending counts
+      const uint32_t t = g;
+      g = l;
+      l = t;
+    }
+    const int x0 = T0 * kTile, x1 = (T0 + J) * kTile;
+    if (x0 < hi) {
+      const uint32_t k0 = (uint32_t)uni((int)key[x0]);
+      g -= k0 >= p ? 1u : 0u;
+      l -= k0 <= p ? 1u : 0u;
+    }
+    if (x1 < hi) {
+      const uint32_t k1 = (uint32_t)uni((int)key[x1]);
+      g += k1 >= p ? 1u : 0u;
+      l += k1 <= p ? 1u : 0u;
+    }
+    cge = (int)g;
+    cle = (int)l;
+  } else if (whole)
     p1_counts<KeyT, JM, true>(key, pos0, J, hi, p, cge, cle);
   else if (nval > 0)
     p1_counts<KeyT, JM, false>(key, pos0, J, hi, p, cge, cle);
@@ -1688,7 +1772,8 @@ template <typename KeyT, int NT, int MAXJ>
 __device__ __forceinline__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, uint16_t* gpos,
                          SelScalars<KeyT>& sc, int k, bool topk, int thr, int cap, int& lo,
                          int& hi, int& depth, int& level, int wave_seg,
-                         uint64_t* acc = nullptr, uint32_t* status = nullptr) {
+                         uint64_t* acc = nullptr, uint32_t* status = nullptr,
+                         const uint32_t* l0cnt = nullptr, bool desc = false) {
   const int tid = (NT == 64) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   while (true) {
     if (lo == k || hi == k) return 0;  // a partition boundary sits at k: the set is final
@@ -1719,26 +1804,28 @@ __device__ __forceinline__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spo
     }
     --depth;
     const int J = (hi - lo - 1 + NT - 1) / NT;
+    // SCORE's level-0 tile counts (plain-norm rows; the first level covers the whole zone)
+    const uint32_t* tc = level == 0 && lo == 0 ? l0cnt : nullptr;
     int cut;
 #ifdef KVC_STAMPS
     const uint64_t tl0 = __builtin_amdgcn_s_memtime();
 #endif
     if (J <= 1)
-      cut = partition_level<KeyT, NT, 1>(key, idx, spos, gpos, sc, lo, hi, cap, acc);
+      cut = partition_level<KeyT, NT, 1>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc, desc);
     else if (J <= 2)
-      cut = partition_level<KeyT, NT, 2>(key, idx, spos, gpos, sc, lo, hi, cap, acc);
+      cut = partition_level<KeyT, NT, 2>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc, desc);
     else if (J <= 4)
-      cut = partition_level<KeyT, NT, 4>(key, idx, spos, gpos, sc, lo, hi, cap, acc);
+      cut = partition_level<KeyT, NT, 4>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc, desc);
     else if (J <= 8)
-      cut = partition_level<KeyT, NT, 8>(key, idx, spos, gpos, sc, lo, hi, cap, acc);
+      cut = partition_level<KeyT, NT, 8>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc, desc);
     else if (MAXJ <= 16 || J <= 16)
-      cut = partition_level<KeyT, NT, 16>(key, idx, spos, gpos, sc, lo, hi, cap, acc);
+      cut = partition_level<KeyT, NT, 16>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc, desc);
     else if (J <= 32)
       cut = partition_level<KeyT, NT, (MAXJ < 32 ? 16 : 32)>(key, idx, spos, gpos, sc, lo, hi, cap,
-                                                               acc);
+                                                               acc, tc, desc);
     else
       cut = partition_level<KeyT, NT, (MAXJ < 64 ? 16 : 64)>(key, idx, spos, gpos, sc, lo, hi, cap,
-                                                               acc);
+                                                               acc, tc, desc);
 #ifdef KVC_STAMPS
     // per block level (first 8): cycles, and segment length  (slots 16.. of the row)
     if (acc && NT > 64 && tid == 0 && level < 5) {
@@ -2305,8 +2392,9 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
         for (int q = 0; q < 21; ++q) accb[q] = 0;
     }
 #endif
-    const int st = run_chain<KeyT, NT, MAXJ>(key, idx, spos, A.gpos, sc, k, topk, thr, cap, lo,
-                                             hi, depth, level, wave_seg, accb);
+    const int st = run_chain<KeyT, NT, MAXJ>(
+        key, idx, spos, A.gpos, sc, k, topk, thr, cap, lo, hi, depth, level, wave_seg, accb,
+        status, ly->score_mode == KVC_SCORE_NORM && MAXJ <= 16 ? trow : nullptr, desc);
     KVC_STAMP(2);
     if (st == 1 && wid == 0)
       run_chain<KeyT, 64, 16>(key, idx, spos, A.gpos, sc, k, topk, thr, cap, lo, hi, depth,
@@ -3278,8 +3366,10 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
     off = round_up(off + (size_t)rows * info->index_row_stride * 4, 256);
     if (max_zone > kZoneMax)  // selection scratch rows for zones longer than the LDS limit
       off += (size_t)rows * sel_scratch_row_bytes((int)info->norm_row_stride, p->dtype);
-    // snapkv rows: SCORE's per-64-token-tile norm maxima (u32 each; tmax_offset())
-    if (snap) off += (size_t)rows * (size_t)(info->norm_row_stride / kTile) * 4;
+    // SCORE's per-64-token-tile statistics (u32 each; tmax_offset()): the norm maximum of a
+    // snapkv row's tile, level 0's ge / le counts of a plain-norm row's tile
+    if (snap || (kL0TileCounts && max_zone > 0))
+      off += (size_t)rows * (size_t)(info->norm_row_stride / kTile) * 4;
 #ifdef KVC_STAMPS
     off += (size_t)rows * 256;  // diagnostic stamp slots (32 x u64 per select row)
 #endif
@@ -3446,8 +3536,10 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
   const bool ext = p->external_index != 0;
   uint32_t* status = p->device_status;
   // snapkv rows: SCORE's per-tile norm maxima (plan_impl reserved them), read by the selection
-  uint32_t* tmax = snap && !ext ? reinterpret_cast<uint32_t*>(w + tmax_offset(info, p->dtype))
-                                : nullptr;
+  uint32_t* tmax = (snap || (kL0TileCounts && info.norm_row_stride > 0)) && !ext
+                       ? reinterpret_cast<uint32_t*>(w + tmax_offset(info, p->dtype))
+                       : nullptr;
+  uint32_t* tmax_sel = tmax;  // snapkv rows read their maxima, plain rows their level-0 counts
   int rc = KVC_OK;
   if ((p->phases & KVC_PHASE_SCORE) && tile_end > tile_base && !ext)
     rc = launch_score<DT, NC>(T, cn, H, tile_base, tile_end - tile_base, norms, nstride, tmax, s);
@@ -3468,7 +3560,7 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
           return launch_k(select_gather_kernel<KC, kSelThreadsSmall, NC, ST>, rows_grid,
                           dim3(kSelThreadsSmall), sel_bytes(n_cap, ks, cap), s, T, H, BH, DT,
                           p->order, p->algo, norms, nstride, kWaveSegSmall, n_cap, cap, status, 0,
-                          tmax);
+                          tmax_sel);
         }
         // fewer rows than CUs (e.g. 4 layers per GPU of an 8-way layer split): one row per CU
         // and idle CUs -- the sink / tail rows get copy-only workgroups of their own
@@ -3479,14 +3571,14 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
         return launch_k(select_gather_kernel<KC, kSelThreads, NC, ST>,
                         dim3((unsigned)(split ? 2 * rows : rows)), dim3(kSelThreads), 0, s, T, H,
                         BH, DT, p->order, p->algo, norms, nstride, kWaveSeg, n_cap, 0, status,
-                        split, tmax);
+                        split, tmax_sel);
       };
       return p->algo == KVC_ALGO_STABLE ? go(std::true_type()) : go(std::false_type());
     }
     char* scratch = w + round_up(info.index_offset + (size_t)info.rows * istride * 4, 256);
     uint64_t* st = stamps ? stamps + (size_t)layers[c0].row0 * 32 : nullptr;
     rc = launch_select<KC>(T, cn, BH, DT, p->order, p->algo, norms, nstride, idx, istride,
-                           long_zone, scratch, st, status, s, tmax);
+                           long_zone, scratch, st, status, s, tmax_sel);
   }
   if (rc != KVC_OK) return rc;
   if ((p->phases & KVC_PHASE_GATHER) && max_part > 0)

@@ -146,7 +146,8 @@ def test_plan_long_zone_gets_global_scratch():
     row += -row % 256
     idx_end = i1.index_offset + 32 * i1.index_row_stride * 4
     idx_end += -idx_end % 256
-    assert i1.workspace_bytes == idx_end + 32 * row
+    tiles = 32 * (n_cap // 64) * 4  # SCORE's per-tile statistics (level-0 counts), round 6
+    assert i1.workspace_bytes == idx_end + 32 * row + tiles
 
 
 def test_plan_zone_beyond_u16_positions_gets_u32_scratch():
@@ -160,7 +161,8 @@ def test_plan_zone_beyond_u16_positions_gets_u32_scratch():
     row += -row % 256
     idx_end = info.index_offset + 32 * info.index_row_stride * 4
     idx_end += -idx_end % 256
-    assert info.workspace_bytes == idx_end + 32 * row
+    tiles = 32 * (n_cap // 64) * 4  # SCORE's per-tile statistics (level-0 counts), round 6
+    assert info.workspace_bytes == idx_end + 32 * row + tiles
 
 
 def test_status_strings():
@@ -295,9 +297,10 @@ def test_device_status_bits_match_header():
     assert all(name.split()[0] in vals for _, name in E._STATUS_BITS)
 
 
-def test_snapkv_calls_reserve_the_tile_maxima_region():
-    """kvc_plan reserves rows x norm_row_stride / 64 u32 after the index region when a layer
-    scores with snapkv (SCORE's per-tile norm maxima, round 6), and nothing for plain norms."""
+def test_scored_calls_reserve_the_tile_statistics_region():
+    """kvc_plan reserves rows x norm_row_stride / 64 u32 after the index region for SCORE's
+    per-tile statistics (round 6): a snapkv row's tile norm maxima, a plain-norm row's level-0
+    ge / le counts -- the same size either way, and nothing for a call that selects nothing."""
     H, D = 4, 64
 
     def plan(mode):
@@ -312,4 +315,7 @@ def test_snapkv_calls_reserve_the_tile_maxima_region():
         assert rc == 0
         return info
     a, b = plan(0), plan(1)
-    assert b.workspace_bytes - a.workspace_bytes == b.rows * (b.norm_row_stride // 64) * 4
+    assert a.workspace_bytes == b.workspace_bytes
+    region = b.rows * (b.norm_row_stride // 64) * 4
+    idx_end = b.index_offset + b.rows * b.index_row_stride * 4
+    assert b.workspace_bytes == -(-idx_end // 256) * 256 + region
