@@ -376,8 +376,8 @@ __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int t
   // std::__move_median_to_first picks it (partition_level) -- by loading those three token rows
   // (L2 hits after their first wave) and computing their norms in torch.norm's order, then
   // counts its tile's keys >= / <= that pivot (ascending keys; a descending selection swaps the
-  // two) and stores ge | le << 16.  Free: the stream is HBM-bound (SCORE 0.6164-0.6194 vs
-  // 0.6164-0.6201 ms, profiles/r06_e_l0_counts_ab.jsonl).
+  // two) and stores ge | le << 16.  Free: the stream is HBM-bound (SCORE 0.613-0.619 ms with,
+  // 0.619-0.623 without, profiles/r06_e_l0_counts_ab.jsonl).
   if constexpr (kL0TileCounts) if (ly->score_mode == KVC_SCORE_NORM && tmax && zlen > 2) {
     const int ptok[3] = {1, zlen / 2, zlen - 1};
     const char* zb = static_cast<const char*>(ly->k) +
@@ -1480,7 +1480,8 @@ template <typename KeyT, int NT, int JM>
 __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_t* spos,
                                                uint16_t* gpos, SelScalars<KeyT>& sc, int lo,
                                                int hi, int cap, uint64_t* acc,
-                                               const uint32_t* tcnt = nullptr, bool desc = false) {
+                                               bool use_tc = false, uint32_t tcv = 0,
+                                               bool desc = false) {
   constexpr int NW = NT / 64;
   typedef typename std::conditional<(JM > 32), uint64_t, uint32_t>::type MaskT;
   const int lane = threadIdx.x & 63;
@@ -1515,15 +1516,16 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
   KVC_TICK(ta);
   // ---- P1: wave ge / le counts ----
   int cge = 0, cle = 0;
-  if (tcnt) {
+  if (use_tc) {
     // level 0 of a plain-norm row (lo = 0, hi = n): SCORE counted every 64-token tile against
     // this pivot (score_tile).  This stripe [wbeg, wbeg + 64 J), wbeg = 1 + 64 T0, is tiles
     // T0 .. T0 + J - 1 without position 64 T0 (the previous stripe's last, or the pivot slot lo)
     // and with position 64 (T0 + J) (its own last, in the next tile).  Same counts as the pass
     // below, including slot ch counted with the pivot's key (corrected for the median move).
-    const int T0 = wid * J, nt = (hi + kTile - 1) / kTile;
-    const uint32_t c = lane < J && T0 + lane < nt ? tcnt[T0 + lane] : 0u;
-    const uint32_t sum = (uint32_t)__builtin_amdgcn_readlane(row_scan16((int)c), 15);
+    // tcv: lane l < J holds tile T0 + l's counts (loaded at the start of select_body, its
+    // latency under the key load)
+    const int T0 = wid * J;
+    const uint32_t sum = (uint32_t)__builtin_amdgcn_readlane(row_scan16((int)tcv), 15);
     uint32_t g = sum & 0xFFFFu, l = sum >> 16;
     if (desc) {  // descending keys are complemented: ge <-> le of the ascending counts
       const uint32_t t = g;
@@ -1773,7 +1775,7 @@ __device__ __forceinline__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spo
                          SelScalars<KeyT>& sc, int k, bool topk, int thr, int cap, int& lo,
                          int& hi, int& depth, int& level, int wave_seg,
                          uint64_t* acc = nullptr, uint32_t* status = nullptr,
-                         const uint32_t* l0cnt = nullptr, bool desc = false) {
+                         bool l0use = false, uint32_t l0tc = 0, bool desc = false) {
   const int tid = (NT == 64) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   while (true) {
     if (lo == k || hi == k) return 0;  // a partition boundary sits at k: the set is final
@@ -1805,27 +1807,32 @@ __device__ __forceinline__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spo
     --depth;
     const int J = (hi - lo - 1 + NT - 1) / NT;
     // SCORE's level-0 tile counts (plain-norm rows; the first level covers the whole zone)
-    const uint32_t* tc = level == 0 && lo == 0 ? l0cnt : nullptr;
+    const bool tc = l0use && level == 0 && lo == 0;
     int cut;
 #ifdef KVC_STAMPS
     const uint64_t tl0 = __builtin_amdgcn_s_memtime();
 #endif
     if (J <= 1)
-      cut = partition_level<KeyT, NT, 1>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc, desc);
+      cut = partition_level<KeyT, NT, 1>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc,
+                                         l0tc, desc);
     else if (J <= 2)
-      cut = partition_level<KeyT, NT, 2>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc, desc);
+      cut = partition_level<KeyT, NT, 2>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc,
+                                         l0tc, desc);
     else if (J <= 4)
-      cut = partition_level<KeyT, NT, 4>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc, desc);
+      cut = partition_level<KeyT, NT, 4>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc,
+                                         l0tc, desc);
     else if (J <= 8)
-      cut = partition_level<KeyT, NT, 8>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc, desc);
+      cut = partition_level<KeyT, NT, 8>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc,
+                                         l0tc, desc);
     else if (MAXJ <= 16 || J <= 16)
-      cut = partition_level<KeyT, NT, 16>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc, desc);
+      cut = partition_level<KeyT, NT, 16>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc,
+                                          l0tc, desc);
     else if (J <= 32)
       cut = partition_level<KeyT, NT, (MAXJ < 32 ? 16 : 32)>(key, idx, spos, gpos, sc, lo, hi, cap,
-                                                               acc, tc, desc);
+                                                               acc, tc, l0tc, desc);
     else
       cut = partition_level<KeyT, NT, (MAXJ < 64 ? 16 : 64)>(key, idx, spos, gpos, sc, lo, hi, cap,
-                                                               acc, tc, desc);
+                                                               acc, tc, l0tc, desc);
 #ifdef KVC_STAMPS
     // per block level (first 8): cycles, and segment length  (slots 16.. of the row)
     if (acc && NT > 64 && tid == 0 && level < 5) {
@@ -2259,6 +2266,16 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
   const bool topk = algo == KVC_ALGO_TOPK;
   const bool partial = topk && (int64_t)k * 64 <= n;  // aten TopKImpl.h: use_partial_sort
   const int thr = topk ? 3 : 16;  // introselect / introsort segment threshold
+  // SCORE's level-0 tile counts of a plain-norm row (score_tile), loaded now so that the load's
+  // latency passes under the key load: lane l < J0 of wave w holds tile w J0 + l, J0 = level 0's
+  // positions per lane (partition_level)
+  const bool l0use = kL0TileCounts && !STABLE && MAXJ <= 16 && trow &&
+                     ly->score_mode == KVC_SCORE_NORM;
+  uint32_t l0tc = 0;
+  if (l0use) {
+    const int J0 = (n - 1 + NT - 1) / NT, t = wid * J0 + lane;
+    l0tc = lane < J0 && t < (n + kTile - 1) / kTile ? trow[t] : 0u;
+  }
 
   // ---- keys ----
   if (ly->score_mode == KVC_SCORE_SNAPKV) {
@@ -2392,9 +2409,9 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
         for (int q = 0; q < 21; ++q) accb[q] = 0;
     }
 #endif
-    const int st = run_chain<KeyT, NT, MAXJ>(
-        key, idx, spos, A.gpos, sc, k, topk, thr, cap, lo, hi, depth, level, wave_seg, accb,
-        status, ly->score_mode == KVC_SCORE_NORM && MAXJ <= 16 ? trow : nullptr, desc);
+    const int st = run_chain<KeyT, NT, MAXJ>(key, idx, spos, A.gpos, sc, k, topk, thr, cap, lo,
+                                             hi, depth, level, wave_seg, accb, status, l0use,
+                                             l0tc, desc);
     KVC_STAMP(2);
     if (st == 1 && wid == 0)
       run_chain<KeyT, 64, 16>(key, idx, spos, A.gpos, sc, k, topk, thr, cap, lo, hi, depth,
