@@ -89,6 +89,21 @@ constexpr bool kSgNtl = KVC_SG_NTL;
 #define KVC_L0_TILE_COUNTS 1
 #endif
 constexpr bool kL0TileCounts = KVC_L0_TILE_COUNTS;
+// Level 0 of a 1 024-thread row with 16-bit keys keeps its rank tables in the idx region (the
+// indices are still the identity there, rebuilt after the swaps): room for every rank a level
+// can need, so no second rank window (partition_level); 0: the shared windows (A/B)
+#ifndef KVC_L0_ITAB
+#define KVC_L0_ITAB 1
+#endif
+constexpr bool kL0Itab = KVC_L0_ITAB;
+// Smallest positions-per-lane bound a level body is specialised on: levels with J <= this run in
+// that body (1: one body per power of two up to 16).  2 folds the J = 1 levels into the J = 2
+// body -- less code for the instruction cache; 1 / 2 / 4 / 8 measured within noise of each other
+// (profiles/r06_f_itab_ab.jsonl)
+#ifndef KVC_LEVEL_JM_MIN
+#define KVC_LEVEL_JM_MIN 2
+#endif
+constexpr int kLevelJmMin = KVC_LEVEL_JM_MIN;
 // SELECT_GATHER rows touch the rows they already know they keep while wave 0 finishes the chain
 // (select_body; diagnostic A/B, off)
 #ifndef KVC_SG_PREFETCH
@@ -1133,10 +1148,17 @@ __device__ __forceinline__ void unroll_for(F&& f) {
 // selection 2 % (SELECT_GATHER 0.1525 -> 0.1494 ms at the headline, 0.187 -> 0.183 snapkv,
 // 0.128 -> 0.124 h2o; profiles/r03_zz_valu_counts_ab.jsonl): the kernel is bound by the CU's
 // total issue work and the scalar unit carried the larger share.
-// WHOLE: every position of the stripe is below hi (unclamped loads with immediate offsets; rows j >= J of a JM-row body read at most
-// JM/2 rows past the stripe, inside the selection arrays).  Otherwise loads are clamped and
-// lanes past hi masked off.  Position ch is counted with the key it holds (the pivot value);
-// the caller corrects the owner wave's counts for the virtual median move.
+// WHOLE: every position of the stripe is below hi (unclamped loads with immediate offsets; rows
+// j >= J of a JM-row body read at most JM/2 rows past the stripe -- the smallest body, 1 --
+// inside the selection arrays).  Otherwise loads are clamped and lanes past hi masked off.
+// Position ch is counted with the key it holds (the pivot value); the caller corrects the owner
+// wave's counts for the virtual median move.
+// A level body of bound JM runs levels with JM/2 < J <= JM, so rows j < JM/2 need no J check --
+// except the smallest body (kLevelJmMin), which runs every J <= JM
+template <int JM>
+__device__ constexpr int jm_rows_past() {
+  return JM <= kLevelJmMin ? 1 : JM / 2;
+}
 template <typename KeyT, int JM, bool WHOLE>
 __device__ __forceinline__ void p1_counts(const KeyT* key, int pos0, int J, int hi, uint32_t p,
                                           int& cge, int& cle) {
@@ -1154,7 +1176,7 @@ __device__ __forceinline__ void p1_counts(const KeyT* key, int pos0, int J, int 
     unroll_for<0, JB>([&](auto qc) {
       constexpr int q = decltype(qc)::value;
       constexpr int j = j0 + q;
-      if (j >= JM / 2 && j >= J) return;
+      if (j >= jm_rows_past<JM>() && j >= J) return;
       bool ge = (uint32_t)kv[q] >= p, le = (uint32_t)kv[q] <= p;
       if constexpr (!WHOLE) {
         const bool inb = pos0 + j * 64 < hi;
@@ -1279,12 +1301,16 @@ __device__ __forceinline__ int p2_count(uint64_t m) {
   if constexpr (KVC_P2_VBASE) return vpopc(m);
   else return __popcll(m);
 }
-template <typename KeyT, int JM, bool FAST, int MODE = P2_FULL>
+// ISINK: the lane sinks start at spos + ssink / gpos + gsink (level 0's tables in the idx region
+// sink into the shared tables); otherwise they are the 64 entries before each table
+template <typename KeyT, int JM, bool FAST, int MODE = P2_FULL, bool ISINK = false>
 __device__ __forceinline__ void p2_window0(const KeyT* key, uint16_t* spos, uint16_t* gpos,
                                            int lane, int pos0, int wbeg, int J, int hi,
                                            uint32_t p, int ch, bool kge, bool kle, int rge1,
-                                           int rle, int tot_le, int cap, int& nsw) {
+                                           int rle, int tot_le, int cap, int& nsw,
+                                           int ssink = -64, int gsink = -64) {
   static_assert(FAST || MODE == P2_FULL, "partial stripes take the full pass");
+  const int ssl = ISINK ? ssink + lane : lane - 64, gsl = ISINK ? gsink + lane : lane - 64;
   // keys in flight per lane (register budget: 64 VGPRs); 4 and 16 measured the same
   // (profiles/r03_c_p2_keys_in_flight_ab.jsonl)
   constexpr int JB = JM < 8 ? JM : 8;
@@ -1304,7 +1330,7 @@ __device__ __forceinline__ void p2_window0(const KeyT* key, uint16_t* spos, uint
     unroll_for<0, JB>([&](auto qc) {
       constexpr int q = decltype(qc)::value;
       constexpr int j = j0 + q;
-      if (j >= JM / 2 && j >= J) return;
+      if (j >= jm_rows_past<JM>() && j >= J) return;
       const int pj = pos0 + j * 64;
       bool ge = (uint32_t)kv[q] >= p, le = (uint32_t)kv[q] <= p;
       if constexpr (!FAST) {
@@ -1319,12 +1345,12 @@ __device__ __forceinline__ void p2_window0(const KeyT* key, uint16_t* spos, uint
       if constexpr (MODE == P2_LEFT) {
         const uint64_t bg = __builtin_amdgcn_ballot_w64(ge);
         const int a1 = vreg(min(mbcnt(bg, rge1), cap1));
-        gpos[ge ? a1 : lane - 64] = (uint16_t)pj;
+        gpos[ge ? a1 : gsl] = (uint16_t)pj;
         rge1 += p2_count(bg);
       } else if constexpr (MODE == P2_RIGHT) {
         const uint64_t bl = __builtin_amdgcn_ballot_w64(le);
         const int sr = vreg(min(t1 - 1 - mbcnt(bl, rle), cap1));  // s rank of an le position
-        spos[le ? sr : lane - 64] = (uint16_t)pj;
+        spos[le ? sr : ssl] = (uint16_t)pj;
         rle += p2_count(bl);
         if (ff == kBig) {
           const uint64_t bg = __builtin_amdgcn_ballot_w64(ge);
@@ -1334,8 +1360,8 @@ __device__ __forceinline__ void p2_window0(const KeyT* key, uint16_t* spos, uint
         const uint64_t bg = __builtin_amdgcn_ballot_w64(ge), bl = __builtin_amdgcn_ballot_w64(le);
         const int a1 = vreg(mbcnt(bg, rge1));                   // g rank: A + 1
         const int sr = vreg(t1 - (mbcnt(bl, rle) + (le ? 1 : 0)));  // s rank: tot_le - Lin + 1
-        spos[le ? min(sr, cap1) : lane - 64] = (uint16_t)pj;
-        gpos[ge ? min(a1, cap1) : lane - 64] = (uint16_t)pj;
+        spos[le ? min(sr, cap1) : ssl] = (uint16_t)pj;
+        gpos[ge ? min(a1, cap1) : gsl] = (uint16_t)pj;
         // g_t < s_t  <=>  A + Lin < tot_le  <=>  a1 < sr: swapped (a prefix t <= m of the g's)
         nsw += __popcll(bg & __builtin_amdgcn_ballot_w64(a1 < sr));
         rge1 += p2_count(bg);
@@ -1476,12 +1502,21 @@ __device__ __forceinline__ void wave_tiny_chain(KeyT* key, uint16_t* idx, int k,
 // positions), so per-position work is a handful of VALU ops: flags are compare ballots
 // (recomputed from the keys in P2 rather than carried), wave counts are scalar popcounts, and
 // wave-uniform work -- median of 3, cross-wave prefix sums, swap count, g_{m+1} -- runs on SGPRs.
-template <typename KeyT, int NT, int JM>
+//
+// ITAB (level 0 of a 1 024-thread row, lo = 0, indices still the identity; ihalf = n_cap / 2):
+// the rank tables are the two halves of the idx region, whose n_cap / 2 - 1 ranks cover every m
+// the level can reach (m <= (hi - lo - 1) / 2): one window.  The median move and P4 then swap keys
+// only; after every table read (a barrier) the indices are rebuilt: the identity with the
+// median's transposition (lo <-> ch), then (another barrier) each swapped pair's entries from
+// the pair kept in registers -- the same arrangement as physical index swaps, without P4's
+// index loads and without the second window (and its flag pass).
+template <typename KeyT, int NT, int JM, bool ITAB = false>
 __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_t* spos,
                                                uint16_t* gpos, SelScalars<KeyT>& sc, int lo,
                                                int hi, int cap, uint64_t* acc,
                                                bool use_tc = false, uint32_t tcv = 0,
-                                               bool desc = false) {
+                                               bool desc = false, int ihalf = 0) {
+  static_assert(!ITAB || (NT > 64 && sizeof(KeyT) == 2), "ITAB: level 0 of 16-bit block rows");
   constexpr int NW = NT / 64;
   typedef typename std::conditional<(JM > 32), uint64_t, uint32_t>::type MaskT;
   const int lane = threadIdx.x & 63;
@@ -1576,26 +1611,52 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
     tot_le = (int)(tot >> 16);
     tot_ge = (int)(tot & 0xFFFFu);
   }
+  // ITAB: the level's tables in the idx region, sinks in the shared tables
+  uint16_t* const shs = spos;
+  bool it = false;
+  int ssink = -64, gsink = -64;
+  if constexpr (ITAB) {
+    it = true;
+    {
+      ssink = (int)(spos - idx);
+      gsink = (int)(gpos - (idx + ihalf));
+      spos = idx;
+      gpos = idx + ihalf;
+      cap = ihalf - 1;
+    }
+  }
   KVC_TICK(t1);
   // ---- P2, rank window 0: s / g rank tables, swap count m, g_{m+1} (stores only) ----
   int nsw = 0;
   if (whole && !owner) {
     if (ge_before + cge + le_before + cle <= tot_le) {  // every ge swapped, no le
-      p2_window0<KeyT, JM, true, P2_LEFT>(key, spos, gpos, lane, pos0, wbeg, J, hi, p, ch, kge,
-                                          kle, ge_before + 1, le_before, tot_le, cap, nsw);
+      p2_window0<KeyT, JM, true, P2_LEFT, ITAB>(key, spos, gpos, lane, pos0, wbeg, J, hi, p, ch,
+                                                kge, kle, ge_before + 1, le_before, tot_le, cap,
+                                                nsw, ssink, gsink);
       nsw = cge;
     } else if (ge_before + le_before >= tot_le) {  // no ge swapped, every le
-      p2_window0<KeyT, JM, true, P2_RIGHT>(key, spos, gpos, lane, pos0, wbeg, J, hi, p, ch, kge,
-                                           kle, ge_before + 1, le_before, tot_le, cap, nsw);
+      p2_window0<KeyT, JM, true, P2_RIGHT, ITAB>(key, spos, gpos, lane, pos0, wbeg, J, hi, p, ch,
+                                                 kge, kle, ge_before + 1, le_before, tot_le, cap,
+                                                 nsw, ssink, gsink);
     } else {
-      p2_window0<KeyT, JM, true>(key, spos, gpos, lane, pos0, wbeg, J, hi, p, ch, kge, kle,
-                                 ge_before + 1, le_before, tot_le, cap, nsw);
+      p2_window0<KeyT, JM, true, P2_FULL, ITAB>(key, spos, gpos, lane, pos0, wbeg, J, hi, p, ch,
+                                                kge, kle, ge_before + 1, le_before, tot_le, cap,
+                                                nsw, ssink, gsink);
     }
   } else if (nval > 0)
-    p2_window0<KeyT, JM, false>(key, spos, gpos, lane, pos0, wbeg, J, hi, p, ch, kge, kle,
-                                ge_before + 1, le_before, tot_le, cap, nsw);
+    p2_window0<KeyT, JM, false, P2_FULL, ITAB>(key, spos, gpos, lane, pos0, wbeg, J, hi, p, ch,
+                                               kge, kle,
+                                ge_before + 1, le_before, tot_le, cap, nsw, ssink, gsink);
   // the median move, made physical by the only wave that reads slot ch (after its P2 loads)
-  if (owner && lane == 0) kv_swap(key, idx, lo, ch);
+  if (owner && lane == 0) {
+    if (ITAB && it) {  // keys only: the idx region holds the tables
+      const KeyT t = key[lo];
+      key[lo] = key[ch];
+      key[ch] = t;
+    } else {
+      kv_swap(key, idx, lo, ch);
+    }
+  }
   int msw;
 #ifdef KVC_STAMPS
   uint64_t tp2 = 0;
@@ -1655,6 +1716,76 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
       wave_sync();
       gnext = ff;
     }
+  }
+  if (ITAB && it) {
+    // ---- P4, one window: the m pairs, ranks t = 1 + tid + q NT (q < JM / 2: m <= NT J / 2),
+    // kept packed (g | s << 16) for the index rebuild; keys swapped now ----
+    constexpr int QM = JM / 2 > 0 ? JM / 2 : 1;
+    // q-rows with a rank for this wave (uniform): the rest keep pr = 0 and touch nothing
+    const int nq = msw >= 1 + wid * 64 ? uni(min(QM, (msw - 1 - wid * 64) / NT + 1)) : 0;
+    uint32_t pr[QM];
+    KeyT kg[QM], ks[QM];
+#pragma unroll
+    for (int q = 0; q < QM; ++q) pr[q] = 0u;
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+      if (q >= nq) break;
+      const int t = 1 + tid + q * NT;
+      const bool v = t <= msw;
+      const int ti = v ? t : 0;
+      const int g = gpos[ti], sv = spos[ti];
+      pr[q] = v ? ((uint32_t)g | (uint32_t)sv << 16) : 0u;  // lo = 0: a self swap of slot 0
+    }
+    // the cut's s_m, read before the tables are overwritten
+    const int sm = msw > 0 ? uni((int)spos[msw]) : kBig;
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+      if (q >= nq) break;
+      kg[q] = key[pr[q] & 0xFFFFu];
+      ks[q] = key[pr[q] >> 16];
+    }
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+      if (q >= nq) break;
+      key[pr[q] & 0xFFFFu] = ks[q];
+      key[pr[q] >> 16] = kg[q];
+    }
+    __syncthreads();  // every table entry is read
+    // identity indices with the median's transposition lo <-> ch: 16-B stores, then the two
+    // entries by the thread that stored them (same-thread LDS order)
+    for (int v = tid; v < (hi + 7) / 8; v += NT) {
+      const uint32_t b = (uint32_t)v * 8;
+      reinterpret_cast<uint4*>(idx)[v] =
+          make_uint4(b | (b + 1) << 16, (b + 2) | (b + 3) << 16, (b + 4) | (b + 5) << 16,
+                     (b + 6) | (b + 7) << 16);
+      if (v == (lo >> 3)) idx[lo] = (uint16_t)ch;
+      if (v == (ch >> 3)) idx[ch] = (uint16_t)lo;
+    }
+    __syncthreads();
+    // the swapped pairs' entries: idx[g] = old idx[s], idx[s] = old idx[g] (old = identity with
+    // lo <-> ch; lo is never swapped).  Lanes without a pair write the shared tables' sinks.
+    uint16_t* sink = shs + lane;
+#pragma unroll
+    for (int q = 0; q < QM; ++q) {
+      if (q >= nq) break;
+      const int g = (int)(pr[q] & 0xFFFFu), sv = (int)(pr[q] >> 16);
+      const bool v = pr[q] != 0u;
+      (v ? idx + g : sink)[0] = (uint16_t)(sv == ch ? lo : sv);
+      (v ? idx + sv : sink)[0] = (uint16_t)(g == ch ? lo : g);
+    }
+    __syncthreads();  // B_c
+    KVC_TICK(t3);
+#ifdef KVC_STAMPS
+    if (acc && tid == 0) {
+      acc[0] += t1 - t0;
+      acc[1] += t2 - t1;
+      acc[2] += t3 - t2;
+      acc[3] += 1;
+      acc[4] += (uint64_t)msw;
+      acc[25] = (t1 - t0) | ((t2 - t1) << 20) | ((t3 - t2) << 40);
+    }
+#endif
+    return min(gnext, sm);
   }
   int wb = 0;
   while (true) {
@@ -1775,7 +1906,8 @@ __device__ __forceinline__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spo
                          SelScalars<KeyT>& sc, int k, bool topk, int thr, int cap, int& lo,
                          int& hi, int& depth, int& level, int wave_seg,
                          uint64_t* acc = nullptr, uint32_t* status = nullptr,
-                         bool l0use = false, uint32_t l0tc = 0, bool desc = false) {
+                         bool l0use = false, uint32_t l0tc = 0, bool desc = false,
+                         int ihalf = 0) {
   const int tid = (NT == 64) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   while (true) {
     if (lo == k || hi == k) return 0;  // a partition boundary sits at k: the set is final
@@ -1812,16 +1944,35 @@ __device__ __forceinline__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spo
 #ifdef KVC_STAMPS
     const uint64_t tl0 = __builtin_amdgcn_s_memtime();
 #endif
-    if (J <= 1)
+    // level 0 of a plain-norm row keeps its rank tables in the idx region (ihalf = n_cap / 2:
+    // n_cap / 2 - 1 ranks per table) when the shared tables could need a second window
+    // (partition_level).  Only those rows: their level-0 swap counts sit around the shared cap
+    // (m median 3 667 of cap 3 840 at the headline: 44 % of rows took a second window), while
+    // the extra barriers and index rebuild measured slower on snapkv rows
+    // (profiles/r06_f_itab_ab.jsonl)
+    const bool itab = kL0Itab && NT == kSelThreads && sizeof(KeyT) == 2 && ihalf > 0 && tc &&
+                      J > 4 && (hi - 1) / 2 > cap && hi <= 2 * ihalf;
+    if constexpr (kL0Itab && NT == kSelThreads && sizeof(KeyT) == 2) {
+      if (itab) {
+        if (J <= 8)
+          cut = partition_level<KeyT, NT, 8, true>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc,
+                                                   l0tc, desc, ihalf);
+        else
+          cut = partition_level<KeyT, NT, 16, true>(key, idx, spos, gpos, sc, lo, hi, cap, acc,
+                                                    tc, l0tc, desc, ihalf);
+      }
+    }
+    if (itab) {
+    } else if (J <= 1 && kLevelJmMin <= 1)
       cut = partition_level<KeyT, NT, 1>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc,
                                          l0tc, desc);
-    else if (J <= 2)
+    else if (J <= 2 && kLevelJmMin <= 2)
       cut = partition_level<KeyT, NT, 2>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc,
                                          l0tc, desc);
-    else if (J <= 4)
+    else if (J <= 4 && kLevelJmMin <= 4)
       cut = partition_level<KeyT, NT, 4>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc,
                                          l0tc, desc);
-    else if (J <= 8)
+    else if (J <= 8 && kLevelJmMin <= 8)
       cut = partition_level<KeyT, NT, 8>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc,
                                          l0tc, desc);
     else if (MAXJ <= 16 || J <= 16)
@@ -1840,6 +1991,7 @@ __device__ __forceinline__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spo
       acc[12 + 2 * level] = acc[25];  // P1 | P2 << 20 | P4 << 40 of this level
     }
 #endif
+    cut = uni(cut);  // uniform by construction; stated, so that lo / hi stay in SGPRs
     // std::__introselect: if (cut <= nth) first = cut; else last = cut;
     // std::__introsort_loop: recurse right, loop on the left part (k <= cut: keep the left).
     // Value selects, not branches: a store through a selected pointer to lo / hi would put
@@ -2411,7 +2563,7 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
 #endif
     const int st = run_chain<KeyT, NT, MAXJ>(key, idx, spos, A.gpos, sc, k, topk, thr, cap, lo,
                                              hi, depth, level, wave_seg, accb, status, l0use,
-                                             l0tc, desc);
+                                             l0tc, desc, MAXJ <= 16 ? n_cap / 2 : 0);
     KVC_STAMP(2);
     if (st == 1 && wid == 0)
       run_chain<KeyT, 64, 16>(key, idx, spos, A.gpos, sc, k, topk, thr, cap, lo, hi, depth,

@@ -140,6 +140,39 @@ def test_abi_select_lengths(S):
         np.testing.assert_array_equal(idx, ref)
 
 
+def _shaped_keys(seed, S, variant, dtype="bf16"):
+    """Rows whose level-0 swap count m spans the range: 'ramp' / 'rramp' (norms rising / falling
+    along the row), 'halves' (the large norms all in the first half: m close to n / 2), else a
+    prng variant ('equal': every position ties, m = (n - 1) / 2 exactly)."""
+    if variant in ("ramp", "rramp", "halves"):
+        K = np.zeros((1, 2, S, 128), dtype=np.float32)
+        r = np.arange(S, dtype=np.float32)
+        col = {"ramp": r + 1.0, "rramp": S - r, "halves": np.where(r < S // 2, 2.0, 1.0)}[variant]
+        K[0, :, :, 0] = col.astype(np.float32)[None, :]
+        K[0, 1, :, 1] = 0.5  # head 1: same order, other values
+        return prng.to_dtype(K, dtype)
+    return prng.gen_keys(seed, (1, 2, S, 128), dtype, variant)
+
+
+@pytest.mark.parametrize("S", [8193, 8194, 9000, 12000, 16383, 16384])
+@pytest.mark.parametrize("variant", ["normal", "few", "equal", "special", "ramp", "rramp", "halves"])
+def test_abi_level0_rank_tables_in_idx_region(S, variant):
+    """Level 0 of 1 024-thread plain-norm rows keeps its rank tables in the idx region and
+    rebuilds the indices after its swaps (partition_level ITAB): every swap count up to the
+    maximum (n - 1) / 2 ('equal', 'halves'), the J = 8 body (S = 8 193) and the J = 9..16 ones,
+    ascending / descending sorts and introselect, against the oracle."""
+    K = _shaped_keys(8800 + S, S, variant)
+    for k in sorted({1, 512, S // 3, S // 2, S - 1}):
+        for desc in (0, 1):
+            nrm, idx = _abi_select(K, k, desc, 0)
+            ref = np.sort(oracle.argsort_prefix(nrm, k, descending=bool(desc)), axis=-1)
+            np.testing.assert_array_equal(idx, ref, err_msg=f"S={S} sort k={k} desc={desc}")
+        if k * 64 > S:  # introselect (k * 64 <= n takes the heap select)
+            nrm, idx = _abi_select(K, k, 1, 1)
+            ref = np.sort(oracle.topk_indices(nrm, k), axis=-1)
+            np.testing.assert_array_equal(idx, ref, err_msg=f"S={S} topk k={k}")
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp16"])
 @pytest.mark.parametrize("variant", ["normal", "few", "equal", "special"])
 def test_abi_decode_tail_selections(dtype, variant):

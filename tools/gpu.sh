@@ -29,6 +29,8 @@
 #   gatherprobe  tools/row_gather_probe (160-B row gathers, load shapes) timed, then FETCH_SIZE
 #              and the TCC read-request counters per shape (one rocprofv3 pass each)
 #                                                                                -> gprobe/
+#   icache:LIB[:WORKLOAD]  SQC instruction-cache + issue counters of SELECT_GATHER with library LIB
+#              on a bench.py workload (default the headline), one rocprofv3 --pmc pass -> ic_*.json
 # Every GPU step runs under its own time limit and the first failure ends the call.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"
@@ -187,6 +189,18 @@ for step in "$@"; do
       done
       python3 tools/pmc_summary.py "$O/sq_${lib}_SQ_WAVE_CYCLES" "$O/sq_${lib}_SQ_LDS_BANK_CONFLICT" > "$O/sq_$lib.json" \
           && cat "$O/sq_$lib.json" ;;
+    icache:*)
+      # icache:LIB[:WORKLOAD] -- instruction-cache and issue counters of SELECT_GATHER (one pass)
+      spec="${step#icache:}"; lib="${spec%%:*}"; wl="fix512-s16384"
+      [ "$spec" != "$lib" ] && wl="${spec#*:}"
+      tag="ic_${lib}_${wl}"
+      ( cd /tmp && export TMPDIR=/tmp && KVC_LIB="$LIBDIR/$lib.so" timeout -s KILL 120 rocprofv3 --pmc \
+          SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_WAVE_CYCLES \
+          SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_WAIT_INST_ANY \
+          --kernel-include-regex "select_gather" --output-format csv -d "$O/$tag" -o run \
+          -- python3 "$R/bench.py" --workload "$wl" --steps 2 --warmup 1 --no-cpu-baseline > "$O/$tag.log" 2>&1 ) \
+          || { tail "$O/$tag.log"; exit 1; }
+      python3 tools/pmc_summary.py "$O/$tag" > "$O/$tag.json" && cat "$O/$tag.json" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
