@@ -86,7 +86,7 @@ constexpr bool kSgNtl = KVC_SG_NTL;
 // (score_tile), which the selection's first partition level sums instead of re-reading the row
 // (partition_level); 0: level 0 counts its keys itself (A/B)
 #ifndef KVC_L0_TILE_COUNTS
-#define KVC_L0_TILE_COUNTS 1
+#define KVC_L0_TILE_COUNTS 0
 #endif
 constexpr bool kL0TileCounts = KVC_L0_TILE_COUNTS;
 // Level 0 of a 1 024-thread row with 16-bit keys keeps its rank tables in the idx region (the
@@ -96,6 +96,14 @@ constexpr bool kL0TileCounts = KVC_L0_TILE_COUNTS;
 #define KVC_L0_ITAB 1
 #endif
 constexpr bool kL0Itab = KVC_L0_ITAB;
+// which rows' level 0 takes the idx-region tables: 0 plain-norm rows, 1 every row (A/B)
+#ifndef KVC_L0_ITAB_ALL
+#define KVC_L0_ITAB_ALL 1
+#endif
+constexpr bool kL0ItabAll = KVC_L0_ITAB_ALL;
+#ifndef KVC_ITAB_COLD
+#define KVC_ITAB_COLD 0
+#endif
 // Smallest positions-per-lane bound a level body is specialised on: levels with J <= this run in
 // that body (1: one body per power of two up to 16).  2 folds the J = 1 levels into the J = 2
 // body -- less code for the instruction cache; 1 / 2 / 4 / 8 measured within noise of each other
@@ -329,6 +337,23 @@ __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int t
   const char* base = static_cast<const char*>(ly->k) +
                      ((int64_t)b * ly->k_stride[0] + (int64_t)h * ly->k_stride[1] +
                       (int64_t)(ly->zone_start + tok0) * ly->k_stride[2]) * ESZ;
+  // plain-norm rows: the three level-0 pivot token rows (see below), loaded before the tile so
+  // that their latency passes under it -- lane u < 3 NC holds row u / NC's chunk u % NC
+  const bool piv = kL0TileCounts && ly->score_mode == KVC_SCORE_NORM && tmax && zlen > 2;
+  constexpr int PV = (3 * NC + 63) / 64;
+  uint4 pvr[PV];
+  if (piv) {
+    const char* zb = static_cast<const char*>(ly->k) +
+                     ((int64_t)b * ly->k_stride[0] + (int64_t)h * ly->k_stride[1] +
+                      (int64_t)ly->zone_start * ly->k_stride[2]) * ESZ;
+#pragma unroll
+    for (int q = 0; q < PV; ++q) {
+      const int u = lane + 64 * q, r = u / NC, c = u - r * NC;
+      const int pt = r == 0 ? 1 : r == 1 ? zlen / 2 : zlen - 1;
+      pvr[q] = u < 3 * NC ? *reinterpret_cast<const uint4*>(zb + pt * sbytes + c * 16)
+                          : make_uint4(0, 0, 0, 0);
+    }
+  }
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ph = 0; ph < NPH; ++ph) {
@@ -388,40 +413,64 @@ __device__ __forceinline__ void score_tile(const kvc_layer_t* ly, int row, int t
   }
   // Plain-norm rows: level 0's P1 counts, per tile (round 6).  Each wave re-derives the row's
   // level-0 pivot -- the median of the keys at zone positions 1, n/2, n-1, as
-  // std::__move_median_to_first picks it (partition_level) -- by loading those three token rows
-  // (L2 hits after their first wave) and computing their norms in torch.norm's order, then
-  // counts its tile's keys >= / <= that pivot (ascending keys; a descending selection swaps the
-  // two) and stores ge | le << 16.  Free: the stream is HBM-bound (SCORE 0.613-0.619 ms with,
-  // 0.619-0.623 without, profiles/r06_e_l0_counts_ab.jsonl).
-  if constexpr (kL0TileCounts) if (ly->score_mode == KVC_SCORE_NORM && tmax && zlen > 2) {
-    const int ptok[3] = {1, zlen / 2, zlen - 1};
-    const char* zb = static_cast<const char*>(ly->k) +
-                     ((int64_t)b * ly->k_stride[0] + (int64_t)h * ly->k_stride[1] +
-                      (int64_t)ly->zone_start * ly->k_stride[2]) * ESZ;
-    // token r's chunk c -> slab row r * NPH + c / CP, column c % CP
-    for (int u = lane; u < 3 * NC; u += 64) {
-      const int r = u / NC, c = u - r * NC;
-      const uint4 x = *reinterpret_cast<const uint4*>(zb + ptok[r] * sbytes + c * 16);
-      *reinterpret_cast<uint4*>(wl + (r * NPH + c / CP) * ROWB + (c % CP) * 16) = x;
+  // std::__move_median_to_first picks it (partition_level) -- from those three token rows (L2
+  // hits after their first wave) with their norms in torch.norm's order, then counts its tile's
+  // keys >= / <= that pivot (ascending keys; a descending selection swaps the two) and stores
+  // ge | le << 16.  bf16 / fp32: one lane per (row, accumulator) runs that accumulator's FMA
+  // chain and the row's lane adds the eight in order (the tile's own lanes run all eight chains
+  // each; a pivot norm on one lane would cost the wave as much VALU work as its whole tile);
+  // fp16's single dim-order accumulator stays on one lane per row.
+  if (piv) {
+#pragma unroll
+    for (int q = 0; q < PV; ++q) {
+      const int u = lane + 64 * q, r = u / NC, c = u - r * NC;
+      if (u < 3 * NC)
+        *reinterpret_cast<uint4*>(wl + (r * NPH + c / CP) * ROWB + (c % CP) * 16) = pvr[q];
     }
     wave_sync();
-    float pa[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (lane < 3) {
+    float ps;
+    constexpr int plane = DT == KVC_F16 ? 1 : 8;  // lane holding row r's norm: plane * r
+    if constexpr (DT == KVC_F16) {
+      float pa[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (lane < 3) {
 #pragma unroll
-      for (int c = 0; c < NC; ++c)
-        accum_chunk<DT, NC>(pa, *reinterpret_cast<const uint4*>(wl + (lane * NPH + c / CP) * ROWB +
-                                                                 (c % CP) * 16), c);
+        for (int c = 0; c < NC; ++c)
+          accum_chunk<DT, NC>(pa, *reinterpret_cast<const uint4*>(wl + (lane * NPH + c / CP) * ROWB +
+                                                                   (c % CP) * 16), c);
+      }
+      ps = pa[0];
+#pragma unroll
+      for (int j = 1; j < 8; ++j) ps = ps + pa[j];
+    } else {
+      // lane 8 r + j: accumulator j of row r -- bf16: element j of every chunk; fp32: element
+      // j & 3 of the chunks c with c & 1 = j >> 2 (accum_chunk's assignment), in chunk order
+      const int r = min(lane >> 3, 2), j = lane & 7;
+      float a = 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        if constexpr (DT == KVC_BF16) {
+          const uint16_t e = *reinterpret_cast<const uint16_t*>(
+              wl + (r * NPH + c / CP) * ROWB + (c % CP) * 16 + j * 2);
+          const float x = bits_to_f32((uint32_t)e << 16);
+          a = __builtin_fmaf(x, x, a);
+        } else {
+          if ((c & 1) != (j >> 2)) continue;
+          const float x = *reinterpret_cast<const float*>(
+              wl + (r * NPH + c / CP) * ROWB + (c % CP) * 16 + (j & 3) * 4);
+          a = __builtin_fmaf(x, x, a);
+        }
+      }
+      ps = a;  // lane 8 r: acc[0] + acc[1] + ... + acc[7], in that order
+#pragma unroll
+      for (int q = 1; q < 8; ++q) ps = ps + __shfl(a, (lane & ~7) + q, 64);
     }
-    float ps = pa[0];
-#pragma unroll
-    for (int j = 1; j < 8; ++j) ps = ps + pa[j];
     const float pr = __builtin_sqrtf(ps);
     uint32_t pk;
     if constexpr (DT != KVC_F32) pk = key16_dt<DT>(bits16_dt<DT>(pr), false);
     else pk = key_f32(f32_to_bits(pr), false);
     const uint32_t ka = (uint32_t)__builtin_amdgcn_readlane((int)pk, 0);
-    const uint32_t kb = (uint32_t)__builtin_amdgcn_readlane((int)pk, 1);
-    const uint32_t kc = (uint32_t)__builtin_amdgcn_readlane((int)pk, 2);
+    const uint32_t kb = (uint32_t)__builtin_amdgcn_readlane((int)pk, plane);
+    const uint32_t kc = (uint32_t)__builtin_amdgcn_readlane((int)pk, 2 * plane);
     const uint32_t p = ka < kb ? (kb < kc ? kb : (ka < kc ? kc : ka))
                                : (ka < kc ? ka : (kb < kc ? kc : kb));
     uint32_t mk;
@@ -1907,7 +1956,7 @@ __device__ __forceinline__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spo
                          int& hi, int& depth, int& level, int wave_seg,
                          uint64_t* acc = nullptr, uint32_t* status = nullptr,
                          bool l0use = false, uint32_t l0tc = 0, bool desc = false,
-                         int ihalf = 0) {
+                         int ihalf = 0, bool l0plain = false) {
   const int tid = (NT == 64) ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
   while (true) {
     if (lo == k || hi == k) return 0;  // a partition boundary sits at k: the set is final
@@ -1950,10 +1999,11 @@ __device__ __forceinline__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spo
     // (m median 3 667 of cap 3 840 at the headline: 44 % of rows took a second window), while
     // the extra barriers and index rebuild measured slower on snapkv rows
     // (profiles/r06_f_itab_ab.jsonl)
-    const bool itab = kL0Itab && NT == kSelThreads && sizeof(KeyT) == 2 && ihalf > 0 && tc &&
-                      J > 4 && (hi - 1) / 2 > cap && hi <= 2 * ihalf;
+    const bool itab = kL0Itab && NT == kSelThreads && sizeof(KeyT) == 2 && ihalf > 0 &&
+                      (l0plain || kL0ItabAll) && level == 0 && lo == 0 && J > 4 &&
+                      (hi - 1) / 2 > cap && hi <= 2 * ihalf;
     if constexpr (kL0Itab && NT == kSelThreads && sizeof(KeyT) == 2) {
-      if (itab) {
+      if (KVC_ITAB_COLD ? __builtin_expect(itab, 0) : itab) {
         if (J <= 8)
           cut = partition_level<KeyT, NT, 8, true>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc,
                                                    l0tc, desc, ihalf);
@@ -2418,16 +2468,13 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
   const bool topk = algo == KVC_ALGO_TOPK;
   const bool partial = topk && (int64_t)k * 64 <= n;  // aten TopKImpl.h: use_partial_sort
   const int thr = topk ? 3 : 16;  // introselect / introsort segment threshold
-  // SCORE's level-0 tile counts of a plain-norm row (score_tile), loaded now so that the load's
-  // latency passes under the key load: lane l < J0 of wave w holds tile w J0 + l, J0 = level 0's
-  // positions per lane (partition_level)
+  // SCORE's level-0 tile counts of a plain-norm row (score_tile), loaded with the keys (below)
+  // so that the load's latency passes under the key load: lane l < J0 of wave w holds tile
+  // w J0 + l, J0 = level 0's positions per lane (partition_level).  Loaded in the plain-norm
+  // branch only: the snapkv scoring keeps the VGPR.
   const bool l0use = kL0TileCounts && !STABLE && MAXJ <= 16 && trow &&
                      ly->score_mode == KVC_SCORE_NORM;
   uint32_t l0tc = 0;
-  if (l0use) {
-    const int J0 = (n - 1 + NT - 1) / NT, t = wid * J0 + lane;
-    l0tc = lane < J0 && t < (n + kTile - 1) / kTile ? trow[t] : 0u;
-  }
 
   // ---- keys ----
   if (ly->score_mode == KVC_SCORE_SNAPKV) {
@@ -2461,6 +2508,10 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
   } else {
     // 16-B loads, all issued before the first use (norm rows are padded to 64 elements, so a
     // whole vector past n stays inside the row); keys/indices written as 16-B LDS stores
+    if (l0use) {
+      const int J0 = (n - 1 + NT - 1) / NT, t = wid * J0 + lane;
+      l0tc = lane < J0 && t < (n + kTile - 1) / kTile ? trow[t] : 0u;
+    }
     constexpr int VEC = 16 / ESZ;
     constexpr int MAXV = ((MAXN < kZoneMax ? MAXN : kZoneMax) / VEC + NT - 1) / NT;  // per batch
     const int nvec = (n + VEC - 1) / VEC;
@@ -2563,7 +2614,8 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
 #endif
     const int st = run_chain<KeyT, NT, MAXJ>(key, idx, spos, A.gpos, sc, k, topk, thr, cap, lo,
                                              hi, depth, level, wave_seg, accb, status, l0use,
-                                             l0tc, desc, MAXJ <= 16 ? n_cap / 2 : 0);
+                                             l0tc, desc, MAXJ <= 16 ? n_cap / 2 : 0,
+                                             !STABLE && ly->score_mode == KVC_SCORE_NORM);
     KVC_STAMP(2);
     if (st == 1 && wid == 0)
       run_chain<KeyT, 64, 16>(key, idx, spos, A.gpos, sc, k, topk, thr, cap, lo, hi, depth,
@@ -3536,8 +3588,9 @@ static int plan_impl(const kvc_params_t* p, kvc_layer_t* layers, int nl, kvc_pla
     if (max_zone > kZoneMax)  // selection scratch rows for zones longer than the LDS limit
       off += (size_t)rows * sel_scratch_row_bytes((int)info->norm_row_stride, p->dtype);
     // SCORE's per-64-token-tile statistics (u32 each; tmax_offset()): the norm maximum of a
-    // snapkv row's tile, level 0's ge / le counts of a plain-norm row's tile
-    if (snap || (kL0TileCounts && max_zone > 0))
+    // snapkv row's tile; for a plain-norm row, level 0's ge / le counts in the KVC_L0_TILE_COUNTS
+    // build (reserved either way: the layout does not depend on the build option)
+    if (snap || max_zone > 0)
       off += (size_t)rows * (size_t)(info->norm_row_stride / kTile) * 4;
 #ifdef KVC_STAMPS
     off += (size_t)rows * 256;  // diagnostic stamp slots (32 x u64 per select row)
