@@ -1950,7 +1950,7 @@ __device__ __forceinline__ int partition_level(KeyT* key, uint16_t* idx, uint16_
 // each level runs a body specialised on its positions-per-lane bound (1..16, or 64 for the
 // global-memory variant of zones longer than kZoneMax).
 // Returns 0 when the first-k set is final, 1 when the block hands a short segment to one wave.
-template <typename KeyT, int NT, int MAXJ>
+template <typename KeyT, int NT, int MAXJ, bool L0T = true>
 __device__ __forceinline__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spos, uint16_t* gpos,
                          SelScalars<KeyT>& sc, int k, bool topk, int thr, int cap, int& lo,
                          int& hi, int& depth, int& level, int wave_seg,
@@ -1999,10 +1999,10 @@ __device__ __forceinline__ int run_chain(KeyT* key, uint16_t* idx, uint16_t* spo
     // (m median 3 667 of cap 3 840 at the headline: 44 % of rows took a second window), while
     // the extra barriers and index rebuild measured slower on snapkv rows
     // (profiles/r06_f_itab_ab.jsonl)
-    const bool itab = kL0Itab && NT == kSelThreads && sizeof(KeyT) == 2 && ihalf > 0 &&
+    const bool itab = L0T && kL0Itab && NT == kSelThreads && sizeof(KeyT) == 2 && ihalf > 0 &&
                       (l0plain || kL0ItabAll) && level == 0 && lo == 0 && J > 4 &&
                       (hi - 1) / 2 > cap && hi <= 2 * ihalf;
-    if constexpr (kL0Itab && NT == kSelThreads && sizeof(KeyT) == 2) {
+    if constexpr (L0T && kL0Itab && NT == kSelThreads && sizeof(KeyT) == 2) {
       if (KVC_ITAB_COLD ? __builtin_expect(itab, 0) : itab) {
         if (J <= 8)
           cut = partition_level<KeyT, NT, 8, true>(key, idx, spos, gpos, sc, lo, hi, cap, acc, tc,
@@ -2433,7 +2433,8 @@ __device__ __forceinline__ void stable_select(const KeyT* key, int n, int k, Sel
 // int32) or, with TO_LDS, to `sel` (LDS u16, may alias the key region: keys are dead by then).
 // Returns false (and ORs KVC_DEV_SELECT_BOUNDS into *status) when the row exceeds this kernel's
 // zone capacity -- nothing is selected then.
-template <int KC, bool TO_LDS, int MAXN, int NT, bool HH = false, bool STABLE = false>
+template <int KC, bool TO_LDS, int MAXN, int NT, bool HH = false, bool STABLE = false,
+          bool L0T = true>
 __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, int dt, int order,
                             int algo, const char* __restrict__ nrow, int32_t* out, uint16_t* sel,
                             char* arrays, int n_cap, int cap,
@@ -2612,10 +2613,9 @@ __device__ __forceinline__ bool select_body(const kvc_layer_t* __restrict__ ly, 
         for (int q = 0; q < 21; ++q) accb[q] = 0;
     }
 #endif
-    const int st = run_chain<KeyT, NT, MAXJ>(key, idx, spos, A.gpos, sc, k, topk, thr, cap, lo,
-                                             hi, depth, level, wave_seg, accb, status, l0use,
-                                             l0tc, desc, MAXJ <= 16 ? n_cap / 2 : 0,
-                                             !STABLE && ly->score_mode == KVC_SCORE_NORM);
+    const int st = run_chain<KeyT, NT, MAXJ, L0T>(
+        key, idx, spos, A.gpos, sc, k, topk, thr, cap, lo, hi, depth, level, wave_seg, accb, status,
+        l0use, l0tc, desc, MAXJ <= 16 ? n_cap / 2 : 0, !STABLE && ly->score_mode == KVC_SCORE_NORM);
     KVC_STAMP(2);
     if (st == 1 && wid == 0)
       run_chain<KeyT, 64, 16>(key, idx, spos, A.gpos, sc, k, topk, thr, cap, lo, hi, depth,
@@ -3164,7 +3164,9 @@ __device__ __forceinline__ void gather_row(const kvc_layer_t* __restrict__ ly, i
 // bound), and the index list never round-trips through global memory.  Layout and thread
 // counts as select_kernel; rows without a selection only copy.
 // ---------------------------------------------------------------------------------------------
-template <int KC, int NT, int NC, bool STABLE = false>
+// L0T: level 0 may keep its rank tables in the idx region (run_chain); the instance without that
+// code runs launches where it does not pay (launch_chunk)
+template <int KC, int NT, int NC, bool STABLE = false, bool L0T = true>
 __global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT))
     select_gather_kernel(const LayerChunk T, int H, int BH, int dt, int order, int algo,
                          const char* __restrict__ norms, int64_t norm_stride, int wave_seg,
@@ -3216,10 +3218,9 @@ __global__ void __launch_bounds__(NT, sel_waves_per_eu(KC, NT))
                      ((int64_t)b * ly->k_stride[0] + (int64_t)h * ly->k_stride[1]) * ESZ;
     const char* pv = static_cast<const char*>(ly->v) +
                      ((int64_t)b * ly->v_stride[0] + (int64_t)h * ly->v_stride[1]) * ESZ;
-    const bool ok = select_body<KC, true, MAXN, NT, false, STABLE>(ly, dt, order, algo, nrow,
-                                                                  nullptr, sel,
-                                                    arrays, n_cap, cap, sc, wave_seg, nullptr,
-                                                    status, trow, pk, pv, NC * 16);
+    const bool ok = select_body<KC, true, MAXN, NT, false, STABLE, L0T>(
+        ly, dt, order, algo, nrow, nullptr, sel, arrays, n_cap, cap, sc, wave_seg, nullptr, status,
+        trow, pk, pv, NC * 16);
     if (!ok) return;  // flagged in *status; the row's output is left unwritten (the copier
                       // workgroup of a split row skips it too)
     __syncthreads();
@@ -3786,14 +3787,27 @@ static int launch_chunk(const kvc_params_t* p, const kvc_plan_info_t& info, cons
         }
         // fewer rows than CUs (e.g. 4 layers per GPU of an 8-way layer split): one row per CU
         // and idle CUs -- the sink / tail rows get copy-only workgroups of their own
-        bool fixed = false;
-        for (int l = c0; l < c0 + cn; ++l)
+        bool fixed = false, plain = false;
+        for (int l = c0; l < c0 + cn; ++l) {
           fixed |= layer_selects(layers[l]) && layers[l].sink_len + layers[l].tail_len > 0;
+          plain |= layer_selects(layers[l]) && layers[l].score_mode == KVC_SCORE_NORM;
+        }
         const int split = fixed && rows <= kSplitCopyRows ? rows : 0;
-        return launch_k(select_gather_kernel<KC, kSelThreads, NC, ST>,
-                        dim3((unsigned)(split ? 2 * rows : rows)), dim3(kSelThreads), 0, s, T, H,
-                        BH, DT, p->order, p->algo, norms, nstride, kWaveSeg, n_cap, 0, status,
-                        split, tmax_sel);
+        const dim3 grid((unsigned)(split ? 2 * rows : rows));
+        // Level 0's idx-region rank tables (run_chain) pay on launches with plain-norm rows;
+        // snapkv-only launches run faster in the instance without that code
+        // (profiles/r06_h_l0t_instance_ab.jsonl: headline snapkv 0.1770 -> 0.1715 ms; with one
+        // row per CU the tables still win for cfg4 ranks, 0.0467 -> 0.0427, and lose 2 us for
+        // cfg5 pyramid ones)
+        if constexpr (!ST) {
+          if (plain)
+            return launch_k(select_gather_kernel<KC, kSelThreads, NC, ST, true>, grid,
+                            dim3(kSelThreads), 0, s, T, H, BH, DT, p->order, p->algo, norms,
+                            nstride, kWaveSeg, n_cap, 0, status, split, tmax_sel);
+        }
+        return launch_k(select_gather_kernel<KC, kSelThreads, NC, ST, false>, grid,
+                        dim3(kSelThreads), 0, s, T, H, BH, DT, p->order, p->algo, norms, nstride,
+                        kWaveSeg, n_cap, 0, status, split, tmax_sel);
       };
       return p->algo == KVC_ALGO_STABLE ? go(std::true_type()) : go(std::false_type());
     }
