@@ -5,7 +5,7 @@ Reports (ms, median of 7), headline geometry [1,32,16384,128] bf16, fix_size_l2 
   * SCORE of 16 layers alone, SELECT_GATHER of 16 layers alone, both on two streams at once;
   * the 32-layer step as one SCORE + one SELECT_GATHER launch, and as a C-chunk pipeline
     (SCORE of every chunk on stream A; SELECT_GATHER of chunk c on stream B after chunk c's
-    SCORE, event-ordered), C = 2, 4, 8."""
+    SCORE, event-ordered), C = 2, 4, 8, with stream B at default and at the highest priority."""
 import json
 import os
 import sys
@@ -49,6 +49,10 @@ def run(tab, phases, stream):
 
 main = torch.cuda.current_stream(dev)
 sa, sb = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+# SELECT_GATHER on a high-priority stream: the dispatcher then places its rows first as SCORE
+# workgroups retire (one 81.5 KB row beside one 74 KB SCORE workgroup fits a CU's 160 KB)
+lo_pri, hi_pri = torch.cuda.Stream.priority_range()
+sbh = torch.cuda.Stream(dev, priority=hi_pri)
 
 
 def timed(fn, reps=7):
@@ -89,7 +93,7 @@ res["score16_and_sg16_two_streams"] = timed(
     lambda: fork_join([(sa, lambda: run(hi, N.PHASE_SCORE, sa)), (sb, lambda: run(lo, SG, sb))]))
 whole = make(range(32))
 res["step32_serial"] = timed(lambda: (run(whole, N.PHASE_SCORE, main), run(whole, SG, main)))
-for C in (2, 4, 8):
+for C, sgs in ((2, sb), (4, sb), (8, sb), (2, sbh), (4, sbh), (8, sbh)):
     tabs = [make(range(c * L // C, (c + 1) * L // C)) for c in range(C)]
 
     def pipe():
@@ -102,12 +106,12 @@ for C in (2, 4, 8):
                 run(tabs[c], N.PHASE_SCORE, sa)
                 e = torch.cuda.Event()
                 e.record(sa)
-            sb.wait_event(e)
-            with torch.cuda.stream(sb):
-                run(tabs[c], SG, sb)
-        for s in (sa, sb):
+            sgs.wait_event(e)
+            with torch.cuda.stream(sgs):
+                run(tabs[c], SG, sgs)
+        for s in (sa, sgs):
             e = torch.cuda.Event()
             e.record(s)
             main.wait_event(e)
-    res[f"step32_pipeline_{C}chunks"] = timed(pipe)
+    res[f"step32_pipeline_{C}chunks" + ("_sg_high_priority" if sgs is sbh else "")] = timed(pipe)
 print(json.dumps(res))
