@@ -657,9 +657,14 @@ __device__ __forceinline__ float div5_rn(float x) {
 // 16-bit scores of positions 8v-8 .. 8v+15 as floats in sw[0..24) (only 8v-2 .. 8v+9 are read;
 // terms outside [hs, he) are skipped): avg_pool1d's window sums in its order, / 5 by div5_rn,
 // rounded to the dtype, mapped to sort keys; positions past n get 0.
+// nonneg (bf16): every score of the row is finite and >= +0 -- the row max is finite, so m >=
+// every norm, and a finite norm is at most sqrt(FLT_MAX) < 2e19, so no whole-window sum (<= 5 m)
+// overflows.  div5_rn's guards then never fire but for r == 0, which only decides the sign of a
+// zero quotient (the keys equate +0 and -0), the division runs as packed fp32 ops, and a value
+// >= +0 maps to key 0x8000 | bits, key_bf16x2's code for it.
 template <int DT>
 __device__ __forceinline__ uint4 snapkv_pool_vec(const float (&sw)[24], int v, int n, bool pool,
-                                                 bool desc) {
+                                                 bool desc, bool nonneg = false) {
   uint32_t o[4] = {0, 0, 0, 0};
   if constexpr (DT == KVC_BF16) {
     // bf16: pairs of positions with packed fp32 adds, one hardware convert and one packed key
@@ -667,6 +672,20 @@ __device__ __forceinline__ uint4 snapkv_pool_vec(const float (&sw)[24], int v, i
     // avg_pool1d's leading 0 + s: it only turns a -0 into +0, and the keys equate the two.
     typedef float f2 __attribute__((ext_vector_type(2)));
     const bool inner = pool && v >= 1 && v * 8 + 10 <= n;  // every window of the vector whole
+    if (inner && nonneg) {
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        f2 acc = f2{sw[2 * p + 6], sw[2 * p + 7]};
+#pragma unroll
+        for (int t = 1; t < 5; ++t) acc = acc + f2{sw[2 * p + 6 + t], sw[2 * p + 7 + t]};
+        const f2 q0 = acc * f2{0.2f, 0.2f};
+        const f2 r = __builtin_elementwise_fma(-q0, f2{5.0f, 5.0f}, acc);
+        const f2 q = __builtin_elementwise_fma(r, f2{0.2f, 0.2f}, q0);
+        const uint32_t k = f32x2_to_bf16x2_hw(q.x, q.y) | 0x80008000u;
+        o[p] = desc ? ~k : k;  // inner: all 8 positions < n
+      }
+      return make_uint4(o[0], o[1], o[2], o[3]);
+    }
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       f2 r;
@@ -774,6 +793,7 @@ __device__ __forceinline__ bool snapkv_keys16(const char* nrow, const uint32_t* 
     const float mx = mb > kInf ? __builtin_nanf("") : in16<DT>(mb);
     // `max + 1e-6` (snapkv_lite.py:99): the python scalar takes the tensor's dtype first
     const float m = in16<DT>(out16<DT>(mx + in16<DT>(out16<DT>(1e-6f))));
+    const bool nonneg = mb < kInf;  // finite max: every score m - norm is finite and >= +0
     KVC_STAMP(26);
     const uint32_t* nw = reinterpret_cast<const uint32_t*>(nrow);
 #pragma unroll
@@ -794,7 +814,7 @@ __device__ __forceinline__ bool snapkv_keys16(const char* nrow, const uint32_t* 
         sw[6 + 2 * d] = in16<DT>(sc6[d] & 0xFFFFu);
         sw[7 + 2 * d] = in16<DT>(sc6[d] >> 16);
       }
-      reinterpret_cast<uint4*>(key)[v] = snapkv_pool_vec<DT>(sw, v, n, pool, desc);
+      reinterpret_cast<uint4*>(key)[v] = snapkv_pool_vec<DT>(sw, v, n, pool, desc, nonneg);
       const uint32_t b = (uint32_t)v * 8;
       reinterpret_cast<uint4*>(idx)[v] =
           make_uint4(b | (b + 1) << 16, (b + 2) | (b + 3) << 16, (b + 4) | (b + 5) << 16,
